@@ -1,0 +1,90 @@
+"""ctypes binding of libsanta_hip.so (the C-ABI declared in include/santa_hip.h).
+
+This is the binding a maintainer of the reference would add.
+There is no fallback: if the shared library is missing the import fails
+loudly, and every device entry point needs a ROCm GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsanta_hip.so")
+
+SH_OK = 0
+SH_ERR_INFEASIBLE = -1
+SH_ERR_ARGS = -2
+SH_ERR_HIP = -3
+SH_MODE_SINGLE = 0
+SH_MODE_TWINS = 1
+SH_COMPAT_TIEBREAK = 1
+SH_MAX_N = 1024
+SH_MAX_N_SANTA = 256
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_U64 = ctypes.c_uint64
+_I64 = ctypes.c_int64
+_U = ctypes.c_uint
+
+# name -> (restype, argtypes); mirrors include/santa_hip.h one to one.
+SIGNATURES = {
+    "sh_last_error": (ctypes.c_char_p, []),
+    "sh_version": (_I, []),
+    "sh_ctx_create": (_I, [ctypes.POINTER(_P), _I, _P, _I, _P, _I, _I, _I, _I]),
+    "sh_ctx_destroy": (None, [_P]),
+    "sh_sample_blocks": (_I, [_U64, _U64, _I, _I, _I, _I, _I, _P, _P]),
+    "sh_solve_blocks": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _U, _P]),
+    "sh_score": (_I, [_P, _P, _P, _P]),
+    "sh_ctx_error_flags": (_I, [_P, _P]),
+    "sh_pack_types": (_I, [_P, _P, _I, _P, _P]),
+    "sh_unpack_types": (_I, [_P, _P, _I, _P, _I, _P]),
+    "lsap_solve_batched_i64": (_I, [_P, _I, _I, _P, _P, _U, _P]),
+    "lsap_solve_batched_i32": (_I, [_P, _I, _I, _P, _P, _U, _P]),
+    "lsap_solve_batched_f64": (_I, [_P, _I, _I, _P, _P, _U, _P]),
+    "lsap_solve_batched_hash": (_I, [_U64, _I64, _I, _I, _P, _P, _U, _P]),
+    "sh_gen_synthetic": (_I, [_U64, _I, _I, _I, _I, _I, _P, _P, _P]),
+}
+
+
+class SantaHipError(RuntimeError):
+    """A C-ABI call returned a negative status."""
+
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where} failed ({code}): {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make -C mpi-hungarian-method_amd/csrc` "
+                "or __graft_entry__.build(); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().sh_last_error().decode(errors="replace")
+
+
+def check(rc: int, where: str) -> int:
+    if rc < 0:
+        msg = last_error()
+        if rc == SH_ERR_INFEASIBLE:
+            raise ValueError(f"cost matrix is infeasible ({where}: {msg})")
+        if rc == SH_ERR_ARGS:
+            raise ValueError(f"{where}: {msg}")
+        raise SantaHipError(rc, where, msg)
+    return rc

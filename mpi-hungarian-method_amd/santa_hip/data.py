@@ -1,0 +1,110 @@
+"""Santa 2017 inputs: the reference's CSV formats and a seeded synthetic generator.
+
+Reference I/O (mpi_single.py:193-196,222-227; mpi_twins.py:199-202,228-229):
+  input/child_wishlist_v2.csv  no header, column 0 = ChildId, then 100 gift ids
+  input/gift_goodkids_v2.csv   no header, column 0 = GiftId, then 1000 child ids
+  baseline_res.csv             header ChildId,GiftId
+The reference drops column 0 with `DataFrame.drop(0, 1)`, a TypeError on
+pandas >= 2; `drop(columns=0)` is the same operation.  Those files are not
+shipped with the reference, so benchmarks use `synthetic()` (same shape).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .sampler import family_sizes
+
+
+@dataclass
+class SantaData:
+    wish: np.ndarray      # int16 [nc, n_wish]   child -> gift ids in preference order
+    goodkids: np.ndarray  # int32 [ng, n_good]   gift  -> child ids in preference order
+    types: np.ndarray     # int16 [nc]           current gift type of every child
+    nq: int               # units per gift type
+
+    @property
+    def nc(self) -> int:
+        return int(self.wish.shape[0])
+
+    @property
+    def ng(self) -> int:
+        return int(self.goodkids.shape[0])
+
+    @property
+    def n_wish(self) -> int:
+        return int(self.wish.shape[1])
+
+    @property
+    def n_good(self) -> int:
+        return int(self.goodkids.shape[1])
+
+    @property
+    def families(self) -> tuple[int, int]:
+        return family_sizes(self.nc)
+
+    def pred(self) -> np.ndarray:
+        """[nc, 2] (ChildId, GiftId) — the `pred` argument of the score."""
+        return np.stack([np.arange(self.nc, dtype=np.int64), self.types.astype(np.int64)], axis=1)
+
+
+def synthetic(seed: int = 2017, nc: int = 1_000_000, ng: int = 1000, nq: int = 1000,
+              n_wish: int = 100, n_good: int = 1000) -> SantaData:
+    """Deterministic Kaggle-shaped data (host C++ generator sh_gen_synthetic)."""
+    wish = np.empty((nc, n_wish), dtype=np.int16)
+    good = np.empty((ng, n_good), dtype=np.int32)
+    types = np.empty(nc, dtype=np.int16)
+    rc = _lib.lib().sh_gen_synthetic(
+        ctypes.c_uint64(seed), nc, ng, nq, n_wish, n_good,
+        wish.ctypes.data_as(ctypes.c_void_p), good.ctypes.data_as(ctypes.c_void_p),
+        types.ctypes.data_as(ctypes.c_void_p))
+    _lib.check(rc, "sh_gen_synthetic")
+    return SantaData(wish, good, types, nq)
+
+
+def read_wishlist(path: str) -> np.ndarray:
+    import pandas as pd
+    return pd.read_csv(path, header=None).drop(columns=0).values.astype(np.int16)
+
+
+def read_goodkids(path: str) -> np.ndarray:
+    import pandas as pd
+    return pd.read_csv(path, header=None).drop(columns=0).values.astype(np.int32)
+
+
+def read_submission(path: str, nc: int | None = None) -> np.ndarray:
+    """baseline_res.csv / improved_sub.csv -> int16 gift type per ChildId."""
+    import pandas as pd
+    sub = pd.read_csv(path)
+    child = sub["ChildId"].to_numpy()
+    gift = sub["GiftId"].to_numpy()
+    n = int(nc if nc is not None else child.max() + 1)
+    types = np.full(n, -1, dtype=np.int16)
+    types[child] = gift
+    if (types < 0).any():
+        raise ValueError(f"{path}: not every child has a gift")
+    return types
+
+
+def write_submission(path: str, types: np.ndarray) -> None:
+    """The reference's checkpoint (mpi_single.py:177,251): ChildId,GiftId."""
+    import pandas as pd
+    pd.DataFrame({"ChildId": np.arange(types.shape[0]), "GiftId": types.astype(np.int64)}).to_csv(
+        path, index=False)
+
+
+def slot_ids(types: np.ndarray, nq: int) -> np.ndarray:
+    """Per-child slot id GiftId*nq + rank within the gift, as
+    `subm.groupby('GiftId').rank() - 1` (method 'average' on ChildId order
+    with unique ranks) builds it at mpi_single.py:224-227."""
+    t = types.astype(np.int64)
+    order = np.lexsort((np.arange(t.shape[0]), t))
+    rank = np.empty_like(t)
+    sorted_t = t[order]
+    starts = np.r_[0, np.flatnonzero(np.diff(sorted_t)) + 1]
+    counts = np.diff(np.r_[starts, sorted_t.shape[0]])
+    rank[order] = np.arange(t.shape[0]) - np.repeat(starts, counts)
+    return t * nq + rank

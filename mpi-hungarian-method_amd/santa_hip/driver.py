@@ -1,0 +1,293 @@
+"""The block-Hungarian round loop — my_optimizer of mpi_single.py:110-182 and
+mpi_twins.py:112-188, one process per GPU.
+
+Per round:
+  sample disjoint blocks (A1) -> every rank solves its shard of the blocks
+  on its GPU, fused cost build + LSAP + apply (A2-A6) -> ranks re-synchronise
+  the gift-type vector with one all-gather (the reference's send/recv +
+  bcast, mpi_single.py:136-152) -> every rank re-scores (A7, :157) ->
+  accept / patience (A8, :160-169).
+
+Semantics kept from the reference:
+  * singles (accept="always"): the new state is always kept — subm_best is
+    an alias of subm at mpi_single.py:113 and current_gift_ids is never
+    reverted — and the loop stops after `patience`+1 consecutive rounds
+    without a new best score (count > 3);
+  * twins (accept="improve"): a round is kept only if the score improves,
+    otherwise rolled back (mpi_twins.py:133,166-175); same stop rule.
+The reference uses `size` blocks per round (one per MPI rank); the default
+here is every disjoint block of the round ("full"), and
+`blocks_per_round=size` reproduces the reference's schedule.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+@dataclass
+class World:
+    rank: int = 0
+    size: int = 1
+    group: object = None
+
+    @property
+    def distributed(self) -> bool:
+        return self.size > 1
+
+
+def shard_range(B: int, rank: int, size: int) -> tuple[int, int, int]:
+    """Blocks [b0, b1) of rank `rank`; every rank gets `per` slots (padded)."""
+    per = (B + size - 1) // size
+    b0 = min(B, rank * per)
+    b1 = min(B, b0 + per)
+    return b0, b1, per
+
+
+def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    import torch.distributed as dist
+    try:
+        dist.all_gather_into_tensor(out, inp, group=group)
+    except (RuntimeError, AttributeError, NotImplementedError):
+        parts = list(out.chunk(dist.get_world_size(group)))
+        dist.all_gather(parts, inp, group=group)
+
+
+@dataclass
+class RoundStats:
+    round: int
+    s_child: int
+    s_gift: int
+    score: float
+    accepted: bool
+    best: float
+    blocks: int
+    seconds: float
+
+
+@dataclass
+class LoopResult:
+    history: list = field(default_factory=list)
+    best_score: float = float("-inf")
+    rounds: int = 0
+    blocks_solved: int = 0
+
+
+def exchange(engine, world: World, mode: int, rows: torch.Tensor, n: int, B: int,
+             types: torch.Tensor, buffers: dict) -> None:
+    """Make every rank's type vector identical after each solved its shard.
+
+    Each rank packs the new types of its own blocks' rows (first twin only
+    for pairs), one all-gather concatenates the shards in rank order (padded
+    to equal size with row id -1), and every rank scatters all of them."""
+    b0, b1, per = shard_range(B, world.rank, world.size)
+    cnt = per * n
+    key = (cnt, world.size)
+    if buffers.get("key") != key:
+        dev = types.device
+        buffers["key"] = key
+        buffers["send"] = torch.full((cnt,), -1, dtype=torch.int16, device=dev)
+        buffers["recv"] = torch.empty((cnt * world.size,), dtype=torch.int16, device=dev)
+        buffers["rows_all"] = torch.full((cnt * world.size,), -1, dtype=torch.int32, device=dev)
+    send, recv, rows_all = buffers["send"], buffers["recv"], buffers["rows_all"]
+    mine = rows[b0 * n:b1 * n]
+    if mine.numel():
+        engine.pack_types(types, mine, send[:mine.numel()])
+    all_gather_flat(recv, send, world.group)
+    # padded layout: rank r's slots hold blocks [r*per, r*per + per) of rows
+    rows_all.fill_(-1)
+    for r in range(world.size):
+        r0, r1, _ = shard_range(B, r, world.size)
+        if r1 > r0:
+            rows_all[r * cnt: r * cnt + (r1 - r0) * n].copy_(rows[r0 * n:r1 * n])
+    engine.unpack_types(types, rows_all, recv, mode)
+
+
+def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, n: int = 256,
+               blocks_per_round: int | None = None, seed: int = 2017, max_rounds: int = 100,
+               accept: str | None = None, patience: int = 3, world: World | None = None,
+               on_round=None, score0: float | None = None) -> LoopResult:
+    """The reference's while-loop; `types` (device int16 [nc]) is updated in place."""
+    world = world or World()
+    accept = accept or ("always" if mode == _lib.SH_MODE_SINGLE else "improve")
+    _, _, _, nb = engine.geometry(mode, n)
+    B = nb if blocks_per_round is None else int(blocks_per_round)
+    if B < 1 or B > nb:
+        raise ValueError(f"blocks_per_round must be in [1, {nb}]")
+    if mode == _lib.SH_MODE_TWINS and blocks_per_round is not None and world.size > nb:
+        # mpi_twins.py:128,132 indexes child_blocks[rank] -> IndexError there
+        raise ValueError(f"{world.size} ranks > {nb} twin blocks per round (the reference "
+                         "raises IndexError at mpi_twins.py:132)")
+    res = LoopResult()
+    if score0 is None:
+        sc, sg, _, _ = engine.score_sums(types)
+        score0 = engine.score_from_sums(sc, sg)
+    best = score0
+    res.best_score = best
+    count = 0
+    buffers: dict = {}
+    backup = torch.empty_like(types) if accept == "improve" else None
+    b0, b1, _ = shard_range(B, world.rank, world.size)
+    for rnd in range(max_rounds):
+        t0 = time.perf_counter()
+        rows = engine.sample_blocks(mode, n, B, seed, rnd)
+        if backup is not None:
+            backup.copy_(types)
+        if b1 > b0:
+            engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types)
+        if world.distributed:
+            exchange(engine, world, mode, rows, n, B, types, buffers)
+        sc, sg, bad_tri, bad_tw = engine.score_sums(types)
+        if bad_tri or bad_tw:
+            raise AssertionError("triplets/twins must share a gift (mpi_single.py:32-44)")
+        score = engine.score_from_sums(sc, sg)
+        improved = score > best
+        if improved:
+            best = score
+            count = 0
+        else:
+            count += 1
+        kept = True
+        if accept == "improve" and not improved:
+            types.copy_(backup)
+            kept = False
+        res.rounds += 1
+        res.blocks_solved += B
+        st = RoundStats(rnd, sc, sg, score, kept, best, B, time.perf_counter() - t0)
+        res.history.append(st)
+        if on_round is not None:
+            on_round(st)
+        if count > patience:
+            break
+    res.best_score = best
+    return res
+
+
+class GPUEngine:
+    """Adapter of SantaGPU to the run_rounds engine protocol."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def geometry(self, mode, n):
+        return self.ctx.geometry(mode, n)
+
+    def sample_blocks(self, mode, n, B, seed, rnd):
+        return self.ctx.sample_blocks(mode, n, B, seed, rnd)
+
+    def solve_blocks(self, mode, rows, n, types):
+        self.ctx.solve_blocks(mode, rows, n, types)
+
+    def pack_types(self, types, rows, out):
+        self.ctx.pack_types(types, rows, out)
+
+    def unpack_types(self, types, rows, vals, mode):
+        self.ctx.unpack_types(types, rows, vals, mode)
+
+    def score_sums(self, types):
+        return self.ctx.score_sums(types)
+
+    def score_from_sums(self, sc, sg):
+        from .context import score_from_sums
+        c = self.ctx
+        return score_from_sums(sc, sg, c.nc, c.ng, c.n_wish, c.n_good)
+
+
+def my_optimizer(subm, score_org, comm=None, rank: int = 0, size: int = 1, gift_data=None,
+                 child_data=None, *, mode: str = "single", block_size: int = 256,
+                 blocks_per_round: int | None = None, seed: int = 2017, max_rounds: int = 100,
+                 patience: int = 3, device: int = 0, verbose: bool = True):
+    """Same call shape as the reference's my_optimizer (mpi_single.py:110).
+
+    subm: DataFrame with ChildId, GiftId; gift_data = good-kids, child_data =
+    wishlists (the reference's names).  `comm` is a torch.distributed
+    process group (or None for one rank).  block_size counts rows: children
+    for singles, twin pairs for twins.  Returns the improved DataFrame."""
+    from .context import SantaGPU
+    ctx = SantaGPU(child_data, gift_data, child_data.shape[0] // gift_data.shape[0], device)
+    types_np = np.full(ctx.nc, -1, dtype=np.int16)
+    types_np[subm["ChildId"].to_numpy()] = subm["GiftId"].to_numpy()
+    types = ctx.upload_types(types_np)
+    m = _lib.SH_MODE_SINGLE if mode == "single" else _lib.SH_MODE_TWINS
+
+    def log(st: RoundStats):
+        if verbose and rank == 0:
+            print("iteration:{} score achieved is: {:.10f}".format(st.round, st.best), flush=True)
+
+    run_rounds(GPUEngine(ctx), types, mode=m, n=block_size, blocks_per_round=blocks_per_round,
+               seed=seed, max_rounds=max_rounds, patience=patience,
+               world=World(rank, size, comm), on_round=log, score0=score_org)
+    out = subm.copy()
+    out["GiftId"] = types.cpu().numpy().astype(np.int64)[out["ChildId"].to_numpy()]
+    return out
+
+
+def main(argv=None) -> int:
+    """CLI of the reference scripts (which take no arguments: every knob was
+    a module global, mpi_single.py:193-240)."""
+    ap = argparse.ArgumentParser(description="MI355X block-Hungarian optimiser (Santa 2017)")
+    ap.add_argument("--mode", choices=["single", "twins"], default="single")
+    ap.add_argument("--block-size", type=int, default=256, help="rows per block (pairs for twins)")
+    ap.add_argument("--blocks-per-round", default="full",
+                    help="'full' (all disjoint blocks), 'ranks' (reference: one per rank) or an int")
+    ap.add_argument("--rounds", type=int, default=20)
+    ap.add_argument("--patience", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=2017)
+    ap.add_argument("--wishlist", help="child_wishlist_v2.csv (default: synthetic data)")
+    ap.add_argument("--goodkids", help="gift_goodkids_v2.csv")
+    ap.add_argument("--init", help="baseline_res.csv / improved_sub.csv to start from")
+    ap.add_argument("--out", default=None, help="write the final submission CSV (rank 0)")
+    ap.add_argument("--synthetic-seed", type=int, default=2017)
+    args = ap.parse_args(argv)
+
+    import os
+    from .context import SantaGPU
+    from . import data as D
+    world = World()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+        world = World(dist.get_rank(), dist.get_world_size(), None)
+    dev = torch.cuda.current_device()
+    if args.wishlist:
+        wish, good = D.read_wishlist(args.wishlist), D.read_goodkids(args.goodkids)
+        types0 = D.read_submission(args.init, wish.shape[0])
+        nq = wish.shape[0] // good.shape[0]
+    else:
+        sd = D.synthetic(args.synthetic_seed)
+        wish, good, types0, nq = sd.wish, sd.goodkids, sd.types, sd.nq
+        if args.init:
+            types0 = D.read_submission(args.init, wish.shape[0])
+    ctx = SantaGPU(wish, good, nq, dev)
+    types = ctx.upload_types(types0)
+    mode = _lib.SH_MODE_SINGLE if args.mode == "single" else _lib.SH_MODE_TWINS
+    bpr = None if args.blocks_per_round == "full" else (
+        world.size if args.blocks_per_round == "ranks" else int(args.blocks_per_round))
+
+    def log(st: RoundStats):
+        if world.rank == 0:
+            print(json.dumps(st.__dict__), flush=True)
+
+    res = run_rounds(GPUEngine(ctx), types, mode=mode, n=args.block_size, blocks_per_round=bpr,
+                     seed=args.seed, max_rounds=args.rounds, patience=args.patience, world=world,
+                     on_round=log)
+    if world.rank == 0:
+        print(json.dumps({"rounds": res.rounds, "blocks": res.blocks_solved,
+                          "best_score": res.best_score}), flush=True)
+        if args.out:
+            D.write_submission(args.out, types.cpu().numpy())
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,67 @@
+"""TEST INFRASTRUCTURE ONLY: a CPU engine for santa_hip.driver.run_rounds built
+on the oracle, so that the driver's host logic (sharding, all-gather
+exchange, accept/rollback, patience) can be tested without a GPU and over
+gloo.  The product engine is santa_hip.driver.GPUEngine."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import torch
+
+import oracle
+from santa_hip import _lib
+from santa_hip.context import score_from_sums
+from santa_hip.sampler import family_sizes, sample_blocks, single_geometry, twin_geometry
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
+
+
+class CPUOracleEngine:
+    def __init__(self, wish, goodkids, nq):
+        self.wish = np.ascontiguousarray(wish, dtype=np.int16)
+        self.good = np.ascontiguousarray(goodkids, dtype=np.int32)
+        self.nc, self.n_wish = self.wish.shape
+        self.ng, self.n_good = self.good.shape
+        self.nq = nq
+        self.n_triplets, self.n_twins = family_sizes(self.nc)
+        self.score_log = []  # (S_child, S_gift, types sha) of every scored state
+
+    def geometry(self, mode, n):
+        if mode == _lib.SH_MODE_SINGLE:
+            lo, count, nb = single_geometry(self.nc, n, self.n_triplets, self.n_twins)
+            return lo, count, 1, nb
+        lo, count, nb = twin_geometry(self.n_triplets, self.n_twins, n)
+        return lo, count, 2, nb
+
+    def sample_blocks(self, mode, n, B, seed, rnd):
+        lo, count, stride, _ = self.geometry(mode, n)
+        return torch.from_numpy(sample_blocks(seed, rnd, lo, count, stride, n, B).reshape(-1).copy())
+
+    def solve_blocks(self, mode, rows, n, types):
+        t = types.numpy()
+        oracle.round_blocks(mode, self.wish, t, rows.numpy().reshape(-1, n), ng=self.ng)
+
+    def pack_types(self, types, rows, out):
+        r = rows.numpy()
+        out.numpy()[:r.shape[0]] = np.where(r >= 0, types.numpy()[np.maximum(r, 0)], -1)
+
+    def unpack_types(self, types, rows, vals, mode):
+        r = rows.numpy()
+        v = vals.numpy()
+        m = r >= 0
+        t = types.numpy()
+        t[r[m]] = v[m]
+        if mode:
+            t[r[m] + 1] = v[m]
+
+    def score_sums(self, types):
+        t = types.numpy()
+        s = oracle.score_sums(self.wish, self.good, t)
+        self.score_log.append((s[0], s[1], sha(t)))
+        return s
+
+    def score_from_sums(self, sc, sg):
+        return score_from_sums(sc, sg, self.nc, self.ng, self.n_wish, self.n_good)

@@ -1,0 +1,265 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the
+reference's golden vectors.  Integer/index results must be bit-exact."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import oracle  # noqa: E402
+from conftest import golden_json  # noqa: E402
+from cpu_engine import sha  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sh():
+    import santa_hip
+    assert torch.cuda.is_available(), "GPU tests need a ROCm GPU"
+    return santa_hip
+
+
+@pytest.fixture(scope="module")
+def ctx(sh, full_data):
+    return sh.SantaGPU.from_data(full_data, 0)
+
+
+# --------------------------------------------------------------------------- LSAP
+def test_lsap_golden_int(sh, lsap_cases):
+    z, meta = lsap_cases
+    by_n = {}
+    for m in meta:
+        if m["kind"] == "int":
+            by_n.setdefault(m["n"], []).append(m)
+    for n, ms in by_n.items():
+        C = np.stack([z[f"C{m['i']}"].astype(np.int64) for m in ms])
+        want = np.stack([z[f"col{m['i']}"].astype(np.int64) for m in ms])
+        for dt in (torch.int64, torch.int32):
+            col, cost = sh.solve_batched(torch.from_numpy(C).to("cuda", dt))
+            assert np.array_equal(col.cpu().numpy(), want), (n, dt)
+            assert cost.cpu().tolist() == [m["cost"] for m in ms]
+        col, _ = sh.solve_batched(torch.from_numpy(C.astype(np.float64)).cuda())
+        assert np.array_equal(col.cpu().numpy(), want), (n, "f64")
+
+
+def test_lsap_golden_float(sh, lsap_cases):
+    z, meta = lsap_cases
+    for m in meta:
+        if not m["kind"].startswith("f64"):
+            continue
+        C = torch.from_numpy(z[f"C{m['i']}"]).cuda()[None]
+        col, cost = sh.solve_batched(C)
+        want = z[f"col{m['i']}"].astype(np.int64)
+        assert np.array_equal(col[0].cpu().numpy(), want), m
+        if m["feasible"]:
+            _, c2 = sh.linear_sum_assignment(z[f"C{m['i']}"])
+            assert np.array_equal(c2, want)
+        else:
+            with pytest.raises(ValueError):
+                sh.linear_sum_assignment(z[f"C{m['i']}"])
+
+
+@pytest.mark.parametrize("n", [64, 128, 256, 512, 1024])
+def test_lsap_random_vs_oracle(sh, n):
+    rng = np.random.default_rng(n)
+    B = 4 if n <= 256 else 2
+    C = rng.integers(0, 1 << 16, size=(B, n, n), dtype=np.int64)
+    col, cost = sh.solve_batched(torch.from_numpy(C).cuda())
+    ocol, ocost = oracle.lsap_i64_batched(C)
+    assert np.array_equal(col.cpu().numpy(), ocol)
+    assert np.array_equal(cost.cpu().numpy(), ocost)
+
+
+@pytest.mark.parametrize("n,mod", [(64, 3), (100, 1 << 16), (256, 1 << 16), (1000, 7)])
+def test_lsap_hash_vs_oracle(sh, n, mod):
+    from santa_hip.sampler import hash_matrix
+    B = 3
+    col, cost = sh.solve_hash(1234, mod, n, B)
+    col = col.cpu().numpy()
+    for b in range(B):
+        C = hash_matrix(1234, b, n, mod)
+        _, oc = oracle.lsap(C)
+        assert np.array_equal(col[b], oc)
+        assert int(cost[b]) == int(C[np.arange(n), oc].sum())
+
+
+# --------------------------------------------------------------------------- sampler
+@pytest.mark.parametrize("mode,n,B", [(0, 256, 3730), (1, 256, 78), (0, 100, 50)])
+def test_sampler_matches_host_mirror(sh, ctx, mode, n, B):
+    from santa_hip.sampler import sample_blocks
+    lo, count, stride, nb = ctx.geometry(mode, n)
+    assert B <= nb
+    rows = ctx.sample_blocks(mode, n, B, 77, 5).cpu().numpy()
+    want = sample_blocks(77, 5, lo, count, stride, n, B).reshape(-1)
+    assert np.array_equal(rows, want)
+    assert np.unique(rows).size == rows.size
+
+
+# --------------------------------------------------------------------------- blocks
+def test_santa_blocks_golden(sh, ctx, full_data, santa_blocks):
+    z, meta = santa_blocks
+    for m in meta:
+        k, n = m["i"], m["n"]
+        rows = torch.from_numpy(z[f"rows{k}"]).cuda()
+        types = ctx.upload_types(full_data.types)
+        col = torch.empty(n, dtype=torch.int32, device="cuda")
+        cost = torch.empty(1, dtype=torch.int64, device="cuda")
+        mode = 0 if m["mode"] == "single" else 1
+        ctx.solve_blocks(mode, rows, n, types, col=col, cost=cost)
+        assert np.array_equal(col.cpu().numpy(), z[f"col{k}"].astype(np.int32)), m
+        assert int(cost.item()) == m["cost_units"], m
+    assert ctx.error_flags() == 0
+
+
+@pytest.mark.parametrize("mode,n,B", [(0, 256, 64), (0, 64, 40), (0, 100, 16), (1, 256, 8),
+                                      (1, 37, 9)])
+def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
+    """Fused build+solve+apply on the GPU equals the CPU oracle: col, exact
+    cost, the whole new type vector, and the happiness deltas."""
+    rows = ctx.sample_blocks(mode, n, B, 2024, 1)
+    types = ctx.upload_types(full_data.types)
+    col = torch.empty(B * n, dtype=torch.int32, device="cuda")
+    cost = torch.empty(B, dtype=torch.int64, device="cuda")
+    delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+    steps = torch.empty(B, dtype=torch.int64, device="cuda")
+    ctx.solve_blocks(mode, rows, n, types, col=col, cost=cost, delta=delta, steps=steps)
+    t_host = full_data.types.copy()
+    st = np.zeros(2, dtype=np.uint64)
+    ocol, ocost = oracle.round_blocks(mode, full_data.wish, t_host, rows.cpu().numpy().reshape(B, n),
+                                      stats=st, ng=full_data.ng)
+    assert np.array_equal(col.cpu().numpy().reshape(B, n), ocol)
+    assert np.array_equal(cost.cpu().numpy(), ocost)
+    assert np.array_equal(types.cpu().numpy(), t_host)
+    assert int(steps.sum()) == int(st[0])
+    s0 = oracle.score_sums(full_data.wish, full_data.goodkids, full_data.types)
+    s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
+    assert delta.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]]
+    assert ctx.error_flags() == 0
+
+
+def test_full_round_properties(sh, ctx, full_data):
+    """BASELINE config 2 at full size (3730 disjoint n=256 blocks): size-
+    independent invariants + exact agreement of delta with a full rescore,
+    and a random 64-block spot check against the oracle."""
+    mode, n = 0, 256
+    _, _, _, nb = ctx.geometry(mode, n)
+    assert nb == 3730
+    rows = ctx.sample_blocks(mode, n, nb, 9, 0)
+    types = ctx.upload_types(full_data.types)
+    cost = torch.empty(nb, dtype=torch.int64, device="cuda")
+    col = torch.empty(nb * n, dtype=torch.int32, device="cuda")
+    delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+    s0 = ctx.score_sums(types)
+    ctx.solve_blocks(mode, rows, n, types, col=col, cost=cost, delta=delta)
+    s1 = ctx.score_sums(types)
+    assert ctx.error_flags() == 0
+    t1 = types.cpu().numpy()
+    # gift multiset conserved, families untouched, every block a permutation
+    assert np.array_equal(np.bincount(t1, minlength=1000), np.bincount(full_data.types, minlength=1000))
+    tri, tw = full_data.families
+    assert np.array_equal(t1[:tri + tw], full_data.types[:tri + tw])
+    c = col.cpu().numpy().reshape(nb, n)
+    assert (np.sort(c, axis=1) == np.arange(n)).all()
+    assert delta.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]]
+    assert s1[2] == 0 and s1[3] == 0
+    # spot-check blocks against the oracle from the same starting state
+    r = rows.cpu().numpy().reshape(nb, n)
+    pick = np.random.default_rng(0).choice(nb, 48, replace=False)
+    t_host = full_data.types.copy()
+    ocol, ocost = oracle.round_blocks(mode, full_data.wish, t_host, r[pick], ng=full_data.ng)
+    assert np.array_equal(c[pick], ocol)
+    assert np.array_equal(cost.cpu().numpy()[pick], ocost)
+    assert np.array_equal(t1[r[pick].reshape(-1)], t_host[r[pick].reshape(-1)])
+
+
+# --------------------------------------------------------------------------- score
+def test_score_matches_golden(sh, ctx, full_data):
+    g = golden_json("santa_score.json")
+    base = g["entries"][0]
+    types = ctx.upload_types(full_data.types)
+    assert ctx.score_sums(types) == (base["S_child"], base["S_gift"], 0, 0)
+    assert ctx.score(types) == base["score"]
+    # a perturbed state vs the oracle, with broken families reported
+    t2 = full_data.types.copy()
+    rng = np.random.default_rng(1)
+    idx = rng.choice(full_data.nc, 5000, replace=False)
+    t2[idx] = rng.integers(0, 1000, 5000)
+    got = ctx.score_sums(ctx.upload_types(t2))
+    want = oracle.score_sums(full_data.wish, full_data.goodkids, t2)
+    assert got == want
+    assert want[2] + want[3] > 0
+    with pytest.raises(AssertionError):
+        ctx.score(ctx.upload_types(t2))
+
+
+def test_avg_normalized_happiness_api(sh, full_data):
+    g = golden_json("santa_score.json")
+    s = sh.avg_normalized_happiness(full_data.pred(), full_data.goodkids, full_data.wish)
+    assert s == g["entries"][0]["score"]
+
+
+# --------------------------------------------------------------------------- driver
+@pytest.mark.parametrize("mode", ["single", "twins"])
+def test_trajectory_gpu_matches_reference(sh, ctx, full_data, mode):
+    from santa_hip.driver import GPUEngine, World, run_rounds
+    g = golden_json(f"trajectory_{mode}.json")
+    types = ctx.upload_types(full_data.types)
+    shas = []
+
+    class Rec(GPUEngine):
+        def score_sums(self, t):
+            shas.append(sha(t.cpu().numpy()))
+            return super().score_sums(t)
+
+    m = 0 if mode == "single" else 1
+    res = run_rounds(Rec(ctx), types, mode=m, n=g["n"], blocks_per_round=g["P"], seed=g["seed"],
+                     max_rounds=g["rounds"], world=World(), score0=g["score0"])
+    assert [st.score for st in res.history] == [r["score"] for r in g["per_round"]]
+    assert shas == [r["types_sha"] for r in g["per_round"]]
+
+
+def test_optimize_block_api(sh, full_data, santa_blocks):
+    from santa_hip import data as D
+    z, meta = santa_blocks
+    sh.init(full_data.wish, full_data.goodkids)
+    slots = D.slot_ids(full_data.types, full_data.nq)
+    import pandas as pd
+    subm = pd.DataFrame({"ChildId": np.arange(full_data.nc), "GiftId": full_data.types.astype(np.int64)})
+    for m in meta[:3] + [x for x in meta if x["mode"] == "twins"][:2]:
+        k = m["i"]
+        blk = z[f"rows{k}"].astype(np.int64)
+        if m["mode"] == "single":
+            cids, gids = sh.optimize_block(blk, slots)
+            assert np.array_equal(gids, slots[blk][z[f"col{k}"]])
+        else:
+            cids, gids = sh.optimize_block_twins(blk, subm)
+            assert np.array_equal(gids, full_data.types[blk][z[f"col{k}"]].astype(np.int64))
+        assert np.array_equal(cids, blk)
+
+
+# --------------------------------------------------------------------------- errors
+def test_error_paths(sh, ctx, full_data):
+    types = ctx.upload_types(full_data.types)
+    bad = torch.full((256,), full_data.nc + 5, dtype=torch.int32, device="cuda")
+    ctx.solve_blocks(0, bad, 256, types)
+    assert ctx.error_flags() & 1
+    assert np.array_equal(types.cpu().numpy(), full_data.types)  # skipped block wrote nothing
+    with pytest.raises(ValueError):
+        ctx.solve_blocks(0, torch.zeros(512, dtype=torch.int32, device="cuda"), 512, types)
+    with pytest.raises(ValueError):
+        ctx.sample_blocks(0, 256, 5000, 1, 0)
+    with pytest.raises(ValueError):
+        sh.linear_sum_assignment(np.array([[np.nan, 0.0], [0.0, 0.0]]))
+
+
+def test_pack_unpack_roundtrip(sh, ctx, full_data):
+    types = ctx.upload_types(full_data.types)
+    rows = ctx.sample_blocks(1, 64, 10, 3, 3)
+    buf = torch.empty(rows.numel(), dtype=torch.int16, device="cuda")
+    ctx.pack_types(types, rows, buf)
+    assert np.array_equal(buf.cpu().numpy(), full_data.types[rows.cpu().numpy()])
+    t2 = torch.zeros_like(types)
+    ctx.unpack_types(t2, rows, buf, 1)
+    r = rows.cpu().numpy()
+    t2n = t2.cpu().numpy()
+    assert np.array_equal(t2n[r], full_data.types[r]) and np.array_equal(t2n[r + 1], full_data.types[r])

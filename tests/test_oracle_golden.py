@@ -1,0 +1,130 @@
+"""The CPU oracle against the reference's golden vectors (no GPU).
+
+Pins the oracle before it is trusted as the GPU path's checker:
+  * lsap_cases.npz     — scipy.optimize.linear_sum_assignment's own col_ind
+                         (tie-heavy ints, reals, +inf) for the SAP restatement;
+  * santa_blocks.npz   — the reference's optimize_block / optimize_block_twins
+                         (mpi_single.py:93-102, mpi_twins.py:93-105);
+  * santa_score.json   — the reference's avg_normalized_happiness
+                         (mpi_single.py:13-83) on the full synthetic instance;
+  * trajectory_*.json  — the reference's my_optimizer run for 3 rounds.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import golden_json
+from cpu_engine import CPUOracleEngine, sha
+from santa_hip import _lib
+from santa_hip.driver import World, run_rounds
+
+
+def test_lsap_int_cases_match_scipy(lsap_cases):
+    z, meta = lsap_cases
+    n_checked = 0
+    for m in meta:
+        if m["kind"] != "int":
+            continue
+        C = z[f"C{m['i']}"].astype(np.int64)
+        want = z[f"col{m['i']}"].astype(np.int64)
+        _, got = oracle.lsap(C)
+        assert np.array_equal(got, want), m
+        _, got_f = oracle.lsap(C.astype(np.float64))
+        assert np.array_equal(got_f, want), m
+        assert int(C[np.arange(C.shape[0]), got].sum()) == m["cost"]
+        n_checked += 1
+    assert n_checked > 100
+
+
+def test_lsap_float_cases_match_scipy(lsap_cases):
+    z, meta = lsap_cases
+    for m in meta:
+        if not m["kind"].startswith("f64"):
+            continue
+        C = z[f"C{m['i']}"]
+        want = z[f"col{m['i']}"].astype(np.int64)
+        if m["feasible"]:
+            _, got = oracle.lsap(C)
+            assert np.array_equal(got, want), m
+            assert C[np.arange(C.shape[0]), got].sum() == m["cost"]
+        else:
+            with pytest.raises(ValueError):
+                oracle.lsap(C)
+
+
+def test_lsap_rejects_nan_and_neginf():
+    with pytest.raises(ValueError):
+        oracle.lsap(np.array([[np.nan, 1.0], [1.0, 2.0]]))
+    with pytest.raises(ValueError):
+        oracle.lsap(np.array([[-np.inf, 1.0], [1.0, 2.0]]))
+
+
+def test_lsap_empty_and_rectangular():
+    r, c = oracle.lsap(np.zeros((0, 0)))
+    assert r.size == 0 and c.size == 0
+    from scipy.optimize import linear_sum_assignment as lsa
+    rng = np.random.default_rng(3)
+    for _ in range(40):
+        C = rng.integers(0, 4, size=(rng.integers(1, 9), rng.integers(1, 9))).astype(float)
+        a, b = lsa(C), oracle.lsap(C)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def _local_block(z, m):
+    """Rebuild a block-local mini instance from the fixture's block data."""
+    k = m["i"]
+    n = m["n"]
+    ctype = z[f"ctype{k}"]
+    if m["mode"] == "single":
+        wish = z[f"wish{k}"]
+        types = ctype.copy()
+        rows = np.arange(n, dtype=np.int32)
+    else:
+        w2 = z[f"wish{k}"]                      # [pairs, 2, n_wish]
+        wish = w2.reshape(2 * n, -1)            # child 2i = first twin, 2i+1 second
+        types = np.repeat(ctype, 2)
+        rows = 2 * np.arange(n, dtype=np.int32)
+    return wish, types, rows
+
+
+def test_santa_blocks_cost_and_assignment(santa_blocks):
+    z, meta = santa_blocks
+    for m in meta:
+        wish, types, rows = _local_block(z, m)
+        fn = oracle.cost_single if m["mode"] == "single" else oracle.cost_twins
+        C = fn(wish, types, rows, ng=1000)
+        _, col = oracle.lsap(C)
+        assert np.array_equal(col, z[f"col{m['i']}"].astype(np.int64)), m
+        assert int(C[np.arange(m["n"]), col].sum()) == m["cost_units"], m
+        # the float64 matrix the reference hands scipy is C * 2^-31 exactly
+        _, col_f = oracle.lsap(C.astype(np.float64) / 2 ** 31)
+        assert np.array_equal(col_f, col)
+
+
+def test_score_matches_reference(full_data):
+    g = golden_json("santa_score.json")
+    assert sha(full_data.wish) == g["data"]["wish_sha"], "synthetic generator drifted"
+    assert sha(full_data.goodkids) == g["data"]["good_sha"]
+    assert sha(full_data.types) == g["data"]["types_sha"]
+    base = g["entries"][0]
+    sc, sg, bt, btw = oracle.score_sums(full_data.wish, full_data.goodkids, full_data.types)
+    assert (sc, sg, bt, btw) == (base["S_child"], base["S_gift"], 0, 0)
+    s = oracle.score_from_sums(sc, sg, full_data.nc, full_data.ng, full_data.n_wish, full_data.n_good)
+    assert s == base["score"]
+
+
+@pytest.mark.parametrize("mode", ["single", "twins"])
+def test_trajectory_matches_reference(full_data, mode):
+    """run_rounds (the product driver) on the CPU oracle engine replays the
+    reference's my_optimizer: same scores, bit for bit, same states."""
+    g = golden_json(f"trajectory_{mode}.json")
+    eng = CPUOracleEngine(full_data.wish, full_data.goodkids, full_data.nq)
+    import torch
+    types = torch.from_numpy(full_data.types.copy())
+    m = _lib.SH_MODE_SINGLE if mode == "single" else _lib.SH_MODE_TWINS
+    res = run_rounds(eng, types, mode=m, n=g["n"], blocks_per_round=g["P"], seed=g["seed"],
+                     max_rounds=g["rounds"], world=World(), score0=g["score0"])
+    assert res.rounds == len(g["per_round"])
+    for st, want, log in zip(res.history, g["per_round"], eng.score_log):
+        assert st.score == want["score"]
+        assert log[2] == want["types_sha"]
