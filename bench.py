@@ -141,16 +141,22 @@ def main():
             self.c.unpack_types(t, r, v, m)
 
     sc0, sg0, _, _ = ctx.score_sums(types)
-    state["best"] = santa_hip.score_from_sums(sc0, sg0, ctx.nc, ctx.ng, ctx.n_wish, ctx.n_good)
+    score0 = santa_hip.score_from_sums(sc0, sg0, ctx.nc, ctx.ng, ctx.n_wish, ctx.n_good)
+    # warm up on the same rounds, then restart from the baseline assignment so
+    # the timed rounds are rounds 0..K-1 of the optimisation (as in the
+    # reference, which starts from baseline_res.csv)
+    state["best"] = score0
     for r in range(args.warmup):
-        step(r, False)
-    score_start = state["best"]
+        step(r % max(args.steps, 1), False)
+    types.copy_(ctx.upload_types(sd.types))
+    state["best"] = score0
+    score_start = score0
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for r in range(args.warmup, args.warmup + args.steps):
+    for r in range(args.steps):
         step(r, True)
     torch.cuda.synchronize()
     if dist:

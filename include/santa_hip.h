@@ -41,6 +41,10 @@ extern "C" {
 #define SH_MODE_TWINS 1  /* rows are first-twin ids c, c+1 (mpi_twins.py)  */
 
 #define SH_COMPAT_TIEBREAK 1u /* scipy's exact tie-break (always on) */
+/* Test/profiling flags (same results, different code path or phases):     */
+#define SH_FLAG_EXACT_ARGMIN 2u /* always use the two-pass exact argmin    */
+#define SH_FLAG_BUILD_ONLY 4u   /* sh_solve_blocks: build the cost tiles and
+                                   apply the identity (phase timing only)  */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024
@@ -118,6 +122,11 @@ int sh_score(sh_ctx *ctx, const int16_t *d_types, int64_t *d_sums, void *stream)
  * range; bit 1: infeasible solve).  Synchronises `stream`; clears the flags. */
 int sh_ctx_error_flags(sh_ctx *ctx, void *stream);
 
+/* Profiling counter: Dijkstra steps of sh_solve_blocks that took the exact
+ * two-pass argmin (cost spreads beyond the packed key's 2^42-unit window, or
+ * SH_FLAG_EXACT_ARGMIN) since the last call.  Synchronises; clears.        */
+int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream);
+
 /* ---------------------------------------------------------------------------
  * Multi-GPU exchange helpers (the reference's comm.send/recv + comm.bcast of
  * results, mpi_single.py:136-147, becomes one RCCL all-gather of these):
@@ -139,6 +148,8 @@ int sh_unpack_types(int16_t *d_types, const int32_t *d_rows, int count,
  *   d_cost [B] (nullable) sum of the chosen entries
  * f64: bit-exact replay of scipy's float64 arithmetic for ANY finite/+inf
  * input (the caller rejects NaN and -inf, as scipy does).
+ * i64: exact for |C| < 2^50 (keeps every dual/distance < 2^62 at n <= 1024);
+ * the caller checks the bound (santa_hip.lsap does).
  * ------------------------------------------------------------------------ */
 int lsap_solve_batched_i64(const int64_t *d_C, int n, int B, int32_t *d_col,
                            int64_t *d_cost, unsigned flags, void *stream);

@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "santa_hip.h"
@@ -220,10 +221,8 @@ __device__ int sap_solve(const int n, Loader &ld, T *__restrict__ u_l,
 //     wish value -2*(n_wish - r), miss float32(1/(2 n_wish)) = E * 2^-31).
 //   twins: uint16 = code(c1) | code(c2) << 8; cost = float32(h1 + h2) in
 //     units, evaluated exactly with integer arithmetic (twin_cost below).
-// Row layout: lane l's K columns are contiguous bytes (one LDS read per lane).
+// Row layout: natural column order, row stride padded to 16 elements.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int slot_of(int j, int K) { return (j & 63) * K + (j >> 6); }
-
 // Exact units of float32(-2a + e) + a*2^32, i.e. E rounded (RNE) to the
 // float32 ulp at magnitude 2a (host re-derives it with real float32 math and
 // rejects a context where they differ).
@@ -256,54 +255,282 @@ __device__ __forceinline__ int64_t single_cost(uint32_t code, int nw1, int64_t E
   return code ? (int64_t)((int)code - nw1) * 4294967296LL : E;
 }
 
-template <int K>
-struct TileU8Loader {
+// ---------------------------------------------------------------------------
+// int64 multi-wave solver (identical decisions to the algorithm above).
+//
+// One workgroup of NW waves owns one n x n instance.  Thread (wave w, lane l)
+// owns columns j = w*64K + k*64 + l (k < K), keeping spc / -v / path /
+// position-in-`remaining` / row4col of its columns in VGPRs, so every SIMD of
+// the CU relaxes a quarter of the row per Dijkstra step.  The argmin of a
+// step is one 64-bit DPP wave-min per wave + one LDS exchange of NW partials
+// (double-buffered, one barrier) over the packed key
+//     [63:21] clamp(spc - minVal + 2^42, 0, 2^43-1)
+//     [20]    cls  = column assigned                (scipy tie order:
+//     [19:10] pkey = assigned ? pos : 1023 - pos     unassigned first, then
+//     [9:0]   aux  = assigned ? row4col : column     last/first position)
+// so the winner's key alone gives the new minVal, the position to drop from
+// `remaining`, and either the next row (assigned) or the sink (unassigned).
+// Among the remaining columns spc >= minVal after a Dijkstra's first step, so
+// the 43-bit window only saturates on spreads > 2^42 units; a saturated
+// winner is re-decided by the exact two-pass argmin (min spc, then min key).
+// Row duals u, row4col, col4row and the path dump live in LDS; the
+// augmentation is a single-lane walk between two barriers.
+// ---------------------------------------------------------------------------
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t x) {
+  const int lo = (int)(uint32_t)x, hi = (int)(uint32_t)(x >> 32);
+  const uint32_t nlo = (uint32_t)__builtin_amdgcn_update_dpp(lo, lo, CTRL, ROWMASK, 0xF, false);
+  const uint32_t nhi = (uint32_t)__builtin_amdgcn_update_dpp(hi, hi, CTRL, ROWMASK, 0xF, false);
+  return ((uint64_t)nhi << 32) | nlo;
+}
+
+__device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Unsigned min over the 64 lanes, wave-uniform result (lane 63 holds it
+// after the row_bcast steps; GFX9 DPP: quad perms, half-row/row mirrors,
+// row_bcast15/31).
+__device__ __forceinline__ uint64_t wave_min_u64_dpp(uint64_t x) {
+  x = umin64(x, dpp_u64<0xB1, 0xF>(x));   // quad_perm [1,0,3,2]
+  x = umin64(x, dpp_u64<0x4E, 0xF>(x));   // quad_perm [2,3,0,1]
+  x = umin64(x, dpp_u64<0x141, 0xF>(x));  // row_half_mirror
+  x = umin64(x, dpp_u64<0x140, 0xF>(x));  // row_mirror
+  x = umin64(x, dpp_u64<0x142, 0xA>(x));  // row_bcast:15 -> rows 1, 3
+  x = umin64(x, dpp_u64<0x143, 0xC>(x));  // row_bcast:31 -> rows 2, 3
+  return readlane_u64(x, 63);
+}
+
+constexpr int KEY_LO_BITS = 21;
+constexpr uint64_t KEY_HI_MAX = (1ull << 43) - 1;
+constexpr int64_t KEY_BIAS = 1ll << 42;
+constexpr uint64_t SIGN64 = 0x8000000000000000ull;
+
+// clamp(spc - minVal + 2^42, 0, 2^43-1) from sb = spc + (2^42 - minVal) in
+// wrapping arithmetic; exact while |spc|, |minVal| < 2^62 (santa_hip.h bounds
+// |C| so that this holds).
+__device__ __forceinline__ uint64_t key_hi_of(uint64_t sb) {
+  return (sb <= KEY_HI_MAX) ? sb : (((int64_t)sb < 0) ? 0 : KEY_HI_MAX);
+}
+
+struct SolveLds {
+  int64_t *u;       // [n]   row duals
+  int16_t *c4r;     // [n]   col4row (the result)
+  int16_t *r4c;     // [n]   row4col
+  int16_t *path;    // [n]   path dump of the visited columns
+  uint64_t *red;    // [2 * NW + 2 * NW]  step partials (double-buffered) + fallback
+};
+
+template <int NW>
+__device__ __forceinline__ uint64_t block_min_u64(uint64_t wmin, uint64_t *slots, int w) {
+  if constexpr (NW == 1) {
+    return wmin;
+  } else {
+    if ((threadIdx.x & 63) == 0) slots[w] = wmin;
+    __syncthreads();
+    uint64_t g = slots[0];
+#pragma unroll
+    for (int q = 1; q < NW; ++q) g = umin64(g, slots[q]);
+    return g;
+  }
+}
+
+template <int NW, int K, typename Loader>
+__device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, int64_t &steps_out,
+                             int &fallbacks, const bool exact) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t INF = INT64_MAX;
+  int64_t spc[K], nv[K];  // nv = -v (column duals, negated)
+  int path[K], pos[K], r4c[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    nv[k] = 0;
+    path[k] = -1;
+  }
+  int64_t steps = 0;
+  int par = 0;
+  for (int cur = 0; cur < n; ++cur) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = w * (WAVE * K) + k * WAVE + lane;
+      spc[k] = INF;
+      pos[k] = (j < n) ? (n - 1 - j) : -1;
+      r4c[k] = (j < n) ? S.r4c[j] : -1;
+    }
+    int nrem = n;
+    int64_t minVal = 0;
+    int i = cur;
+    int sink;
+    for (;;) {
+      ++steps;
+      const int64_t ui = S.u[i];
+      int64_t c[K];
+      ld.load(i, c);
+      const int64_t kU = minVal - ui;
+      const uint64_t kb = (uint64_t)KEY_BIAS - (uint64_t)minVal;
+      uint64_t best = ~0ull;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int j = w * (WAVE * K) + k * WAVE + lane;
+        const bool act = pos[k] >= 0;
+        const int64_t r = c[k] + kU + nv[k];
+        const bool upd = act && (r < spc[k]);
+        spc[k] = upd ? r : spc[k];
+        path[k] = upd ? i : path[k];
+        const uint32_t lo = (r4c[k] < 0)
+                                ? (((uint32_t)(1023 - pos[k]) << 10) | (uint32_t)j)
+                                : ((1u << 20) | ((uint32_t)pos[k] << 10) | (uint32_t)r4c[k]);
+        const uint64_t key = (key_hi_of((uint64_t)spc[k] + kb) << KEY_LO_BITS) | lo;
+        best = umin64(best, act ? key : ~0ull);
+      }
+      uint64_t g = block_min_u64<NW>(wave_min_u64_dpp(best), S.red + par * NW, w);
+      par ^= 1;
+      const uint64_t hi = g >> KEY_LO_BITS;
+      if (exact || hi == 0 || hi == KEY_HI_MAX) {
+        // exact two-pass argmin: min spc (signed), then min key-low among ties
+        uint64_t m = ~0ull;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if (pos[k] >= 0) m = umin64(m, (uint64_t)spc[k] ^ SIGN64);
+        m = block_min_u64<NW>(wave_min_u64_dpp(m), S.red + 2 * NW, w);
+        const int64_t ms = (int64_t)(m ^ SIGN64);
+        uint64_t b2 = ~0ull;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int j = w * (WAVE * K) + k * WAVE + lane;
+          if (pos[k] >= 0 && spc[k] == ms) {
+            const uint32_t lo = (r4c[k] < 0)
+                                    ? (((uint32_t)(1023 - pos[k]) << 10) | (uint32_t)j)
+                                    : ((1u << 20) | ((uint32_t)pos[k] << 10) | (uint32_t)r4c[k]);
+            b2 = umin64(b2, lo);
+          }
+        }
+        g = block_min_u64<NW>(wave_min_u64_dpp(b2), S.red + 3 * NW, w);
+        minVal = ms;
+        ++fallbacks;
+      } else {
+        minVal = minVal + ((int64_t)hi - KEY_BIAS);
+      }
+      const bool assigned = (g >> 20) & 1u;
+      const int pk = (int)((g >> 10) & 1023u);
+      const int aux = (int)(g & 1023u);
+      const int pstar = assigned ? pk : 1023 - pk;
+      const int last = nrem - 1;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int p = pos[k];
+        pos[k] = (p == pstar) ? -1 : ((p == last) ? pstar : p);
+      }
+      --nrem;
+      if (!assigned) {
+        sink = aux;
+        break;
+      }
+      i = aux;
+    }
+    // Dual update (scipy: u[cur] += minVal; u[i] += minVal - spc[col4row[i]]
+    // for the other visited rows; v[j] -= minVal - spc[j] for visited cols)
+    // and path dump of the visited columns.
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = w * (WAVE * K) + k * WAVE + lane;
+      if (j < n && pos[k] < 0) {
+        const int64_t d = minVal - spc[k];
+        nv[k] = nv[k] + d;
+        if (r4c[k] >= 0) S.u[r4c[k]] = S.u[r4c[k]] + d;
+        S.path[j] = (int16_t)path[k];
+      }
+    }
+    if (tid == 0) S.u[cur] = S.u[cur] + minVal;
+    __syncthreads();
+    if (tid == 0) {  // augment along the path from the sink back to cur
+      int j = sink;
+      for (;;) {
+        const int pi = S.path[j];
+        S.r4c[j] = (int16_t)pi;
+        const int t = S.c4r[pi];
+        S.c4r[pi] = (int16_t)j;
+        j = t;
+        if (pi == cur) break;
+      }
+    }
+    __syncthreads();
+  }
+  steps_out = steps;
+}
+
+// ---------------------------------------------------------------------------
+// Row loaders: return row i's costs of this thread's K columns.
+// ---------------------------------------------------------------------------
+template <int NW, int K>
+struct TileU8Loader {  // singles: uint8 rank codes, row stride RS bytes
   const uint8_t *tile;
-  int nw1;
+  int RS, nw1;
   int64_t E;
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
-    const uint8_t *p = tile + (size_t)i * (WAVE * K) + threadIdx.x * K;
-    uint8_t b[K];
-    if constexpr (K == 1) {
-      b[0] = p[0];
-    } else if constexpr (K == 2) {
-      const uint16_t w = *(const uint16_t *)p;
-      b[0] = w & 0xFF; b[1] = w >> 8;
-    } else {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint8_t *p = tile + (size_t)i * RS + w * (WAVE * K) + lane;
 #pragma unroll
-      for (int q = 0; q < K / 4; ++q) {
-        const uint32_t w = ((const uint32_t *)p)[q];
-#pragma unroll
-        for (int z = 0; z < 4; ++z) b[4 * q + z] = (w >> (8 * z)) & 0xFF;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) c[k] = single_cost(b[k], nw1, E);
+    for (int k = 0; k < K; ++k) c[k] = single_cost(p[k * WAVE], nw1, E);
   }
 };
 
-template <int K>
-struct TileU16Loader {
+template <int NW, int K>
+struct TileU16Loader {  // twins: uint16 code pairs, row stride RS elements
   const uint16_t *tile;
-  int nw1;
+  int RS, nw1;
   int64_t E;
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
-    const uint16_t *p = tile + (size_t)i * (WAVE * K) + threadIdx.x * K;
-    uint16_t h[K];
-    if constexpr (K == 1) {
-      h[0] = p[0];
-    } else {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint16_t *p = tile + (size_t)i * RS + w * (WAVE * K) + lane;
 #pragma unroll
-      for (int q = 0; q < K / 2; ++q) {
-        const uint32_t w = ((const uint32_t *)p)[q];
-        h[2 * q] = w & 0xFFFF; h[2 * q + 1] = w >> 16;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) c[k] = twin_cost(h[k], nw1, E);
+    for (int k = 0; k < K; ++k) c[k] = twin_cost(p[k * WAVE], nw1, E);
   }
 };
 
+template <int NW, int K, typename S>
+struct GlobalLoader {  // generic LSAP: rows streamed from global memory
+  const S *base;
+  int n;
+  __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const S *row = base + (size_t)i * n;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = w * (WAVE * K) + k * WAVE + lane;
+      c[k] = (j < n) ? (int64_t)row[j] : 0;
+    }
+  }
+};
+
+template <int NW, int K>
+struct HashLoader {
+  uint64_t seed;
+  int64_t mod;
+  uint64_t b;
+  int n;
+  __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = w * (WAVE * K) + k * WAVE + lane;
+      c[k] = (j < n) ? (int64_t)(sh_hash_cost(seed, b, (uint64_t)i, (uint64_t)j) % (uint64_t)mod) : 0;
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Fused Santa block kernel: one NW-wave workgroup per block.
+//   build: rows -> column gift types -> type->column chains -> rank-code tile
+//   solve: sap_solve_mw over the tile
+//   apply: types[child_i] = old type of column col[i]; exact cost and
+//          happiness deltas (child side from the tile, gift side from the
+//          inverse good-kids CSR).
+// ---------------------------------------------------------------------------
 struct SantaArgs {
   const int32_t *rows;    // [B * n]
   int16_t *types;         // [nc] in/out
@@ -314,9 +541,10 @@ struct SantaArgs {
   const int16_t *wish;    // [nc * n_wish]
   const int32_t *csr_off; // [nc + 1]
   const uint32_t *csr;    // gift << 16 | rank
-  int32_t *err;           // device error flags
+  int32_t *err;           // [0] error flags, [1] exact-argmin fallback steps
   int64_t E;              // miss value in units
   int n, nc, ng, n_wish, n_good;
+  unsigned flags;
 };
 
 __device__ __forceinline__ int64_t gift_happy(const SantaArgs &a, int child, int t) {
@@ -334,127 +562,171 @@ __device__ __forceinline__ int64_t child_happy(uint32_t code, int nw1) {
 
 __host__ __device__ __forceinline__ size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+constexpr int SANTA_NW = 4;
+constexpr int SANTA_WG = SANTA_NW * WAVE;
+
 struct SantaLds {
-  size_t tile, u, rows, ctype, c4r, head, nxt, total;
+  size_t tile, u, rows, ctype, c4r, r4c, path, red, head, nxt, part, total;
+  int RS;
 };
 
-__host__ __device__ __forceinline__ SantaLds santa_lds_layout(int n, int K, int mode, int ng) {
+__host__ __device__ __forceinline__ SantaLds santa_lds_layout(int n, int mode, int ng) {
   SantaLds L;
+  L.RS = (int)r16((size_t)n);  // row stride in elements
   size_t off = 0;
-  L.tile = off; off += r16((size_t)n * WAVE * K * (mode ? 2 : 1));
-  L.u = off;    off += r16((size_t)n * 8);
-  L.rows = off; off += r16((size_t)n * 4);
-  L.ctype = off; off += r16((size_t)WAVE * K * 2);
-  L.c4r = off;  off += r16((size_t)n * 2);
-  L.head = off; off += r16((size_t)ng * 4);
-  L.nxt = off;  off += r16((size_t)n * 2);
+  L.tile = off;  off += r16((size_t)n * L.RS * (mode ? 2 : 1));
+  L.u = off;     off += r16((size_t)n * 8);
+  L.rows = off;  off += r16((size_t)n * 4);
+  L.ctype = off; off += r16((size_t)n * 2);
+  L.c4r = off;   off += r16((size_t)n * 2);
+  L.r4c = off;   off += r16((size_t)n * 2);
+  L.path = off;  off += r16((size_t)n * 2);
+  L.red = off;   off += r16((size_t)4 * SANTA_NW * 8);
+  L.head = off;  off += r16((size_t)ng * 4);
+  L.nxt = off;   off += r16((size_t)n * 2);
+  L.part = off;  off += r16((size_t)SANTA_NW * 3 * 8);
   L.total = off;
   return L;
 }
 
-// One workgroup (= one wave64) per block: build tile -> solve -> apply.
 template <int K, int MODE>
-__global__ __launch_bounds__(WAVE) void santa_block_kernel(SantaArgs a) {
+__global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
   const int n = a.n;
-  const int RS = WAVE * K;
-  const SantaLds L = santa_lds_layout(n, K, MODE, a.ng);
+  const SantaLds L = santa_lds_layout(n, MODE, a.ng);
+  const int RS = L.RS;
   uint8_t *tile8 = smem + L.tile;
-  int64_t *u_l = (int64_t *)(smem + L.u);
   int32_t *rows_l = (int32_t *)(smem + L.rows);
   int16_t *ctype = (int16_t *)(smem + L.ctype);
-  int16_t *c4r_l = (int16_t *)(smem + L.c4r);
   int32_t *head = (int32_t *)(smem + L.head);
   int16_t *nxt = (int16_t *)(smem + L.nxt);
+  int64_t *part = (int64_t *)(smem + L.part);
+  SolveLds S{(int64_t *)(smem + L.u), (int16_t *)(smem + L.c4r), (int16_t *)(smem + L.r4c),
+             (int16_t *)(smem + L.path), (uint64_t *)(smem + L.red)};
 
   // -- rows of this block, range check -----------------------------------
-  bool bad = false;
-  for (int j = lane; j < n; j += WAVE) {
+  int bad = 0;
+  for (int j = tid; j < n; j += SANTA_WG) {
     const int r = a.rows[(size_t)b * n + j];
     bad |= (r < 0) || (r + MODE >= a.nc);
     rows_l[j] = r;
   }
-  if (__any(bad)) {
-    if (lane == 0) atomicOr(a.err, 1);
+  if (__syncthreads_or(bad)) {
+    if (tid == 0) atomicOr(a.err, 1);
     return;
   }
-  for (int t = lane; t < a.ng; t += WAVE) head[t] = -1;
-  __syncthreads();
-  // -- column gift types and type -> column chains ------------------------
-  for (int j = lane; j < RS; j += WAVE) {
-    int16_t ty = -1;
-    if (j < n) {
-      ty = a.types[rows_l[j]];
-      nxt[j] = (int16_t)atomicExch(&head[ty], j);
-    }
-    ctype[j] = ty;
-  }
+  for (int t = tid; t < a.ng; t += SANTA_WG) head[t] = -1;
   {
     uint4 *t4 = (uint4 *)tile8;
     const int n16 = (int)((size_t)n * RS * (MODE ? 2 : 1) / 16);
-    for (int q = lane; q < n16; q += WAVE) t4[q] = make_uint4(0, 0, 0, 0);
+    for (int q = tid; q < n16; q += SANTA_WG) t4[q] = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
-  // -- fill wish ranks: (virtual row, rank) pairs strided over the lanes ---
+  // -- column gift types and type -> column chains ------------------------
+  for (int j = tid; j < n; j += SANTA_WG) {
+    const int16_t ty = a.types[rows_l[j]];
+    nxt[j] = (int16_t)atomicExch(&head[ty], j);
+    ctype[j] = ty;
+  }
+  __syncthreads();
+  // -- fill wish ranks ------------------------------------------------------
+  // Virtual rows = the block's children (twins: both twins of each pair).
+  // Threads stream 8-byte chunks (4 ranks) of the wishlist rows, U loads in
+  // flight each; every wish is looked up in the type -> column chains and its
+  // rank code written into the tile.
   {
     const int nw = a.n_wish;
     const int vrows = n * (MODE ? 2 : 1);
-    int vr = lane / nw, r = lane - (lane / nw) * nw;
-    for (; vr < vrows;) {
+    auto put = [&](int vr, int r, int wgift) {
       const int i = MODE ? (vr >> 1) : vr;
-      const int child = rows_l[i] + (MODE ? (vr & 1) : 0);
-      const int w = a.wish[(size_t)child * nw + r];
-      for (int j = head[w]; j >= 0; j = nxt[j]) {
-        const size_t e = (size_t)i * RS + slot_of(j, K);
+      for (int j = head[wgift]; j >= 0; j = nxt[j]) {
+        const size_t e = (size_t)i * RS + j;
         if (MODE)
           tile8[2 * e + (vr & 1)] = (uint8_t)(r + 1);
         else
           tile8[e] = (uint8_t)(r + 1);
       }
-      r += WAVE;
-      while (r >= nw) { r -= nw; ++vr; }
+    };
+    if ((nw & 3) == 0) {
+      constexpr int U = 4;
+      const int cpr = nw >> 2;  // 8-byte chunks per row
+      const int total = vrows * cpr;
+      int vr = tid / cpr, cc = tid - (tid / cpr) * cpr;
+      for (int base = 0; base < total; base += SANTA_WG * U) {
+        uint2 q[U];
+        int qvr[U], qcc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          qvr[u] = vr;
+          qcc[u] = cc;
+          if (vr < vrows) {
+            const int child = rows_l[MODE ? (vr >> 1) : vr] + (MODE ? (vr & 1) : 0);
+            q[u] = *(const uint2 *)(a.wish + (size_t)child * nw + 4 * cc);
+          }
+          cc += SANTA_WG;
+          while (cc >= cpr) { cc -= cpr; ++vr; }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (qvr[u] < vrows) {
+            const int r0 = 4 * qcc[u];
+            put(qvr[u], r0 + 0, (int16_t)(q[u].x & 0xFFFF));
+            put(qvr[u], r0 + 1, (int16_t)(q[u].x >> 16));
+            put(qvr[u], r0 + 2, (int16_t)(q[u].y & 0xFFFF));
+            put(qvr[u], r0 + 3, (int16_t)(q[u].y >> 16));
+          }
+        }
+      }
+    } else {
+      int vr = tid / nw, r = tid - (tid / nw) * nw;
+      for (; vr < vrows;) {
+        const int child = rows_l[MODE ? (vr >> 1) : vr] + (MODE ? (vr & 1) : 0);
+        put(vr, r, a.wish[(size_t)child * nw + r]);
+        r += SANTA_WG;
+        while (r >= nw) { r -= nw; ++vr; }
+      }
     }
   }
-  for (int i = lane; i < n; i += WAVE) {
-    u_l[i] = 0;
-    c4r_l[i] = -1;
+  for (int i = tid; i < n; i += SANTA_WG) {
+    S.u[i] = 0;
+    S.c4r[i] = -1;
+    S.r4c[i] = -1;
   }
   __syncthreads();
   // -- solve ------------------------------------------------------------------
   int64_t steps = 0;
-  int st;
+  int fallbacks = 0;
   const int nw1 = a.n_wish + 1;
-  if (MODE == 0) {
-    TileU8Loader<K> ld{tile8, nw1, a.E};
-    st = sap_solve<K, int64_t>(n, ld, u_l, c4r_l, steps);
+  const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
+  if (a.flags & SH_FLAG_BUILD_ONLY) {  // phase timing: tile build + apply identity
+    for (int i = tid; i < n; i += SANTA_WG) S.c4r[i] = (int16_t)i;
+    __syncthreads();
+  } else if (MODE == 0) {
+    const TileU8Loader<SANTA_NW, K> ld{tile8, RS, nw1, a.E};
+    sap_solve_mw<SANTA_NW, K>(n, ld, S, steps, fallbacks, exact);
   } else {
-    TileU16Loader<K> ld{(const uint16_t *)tile8, nw1, a.E};
-    st = sap_solve<K, int64_t>(n, ld, u_l, c4r_l, steps);
+    const TileU16Loader<SANTA_NW, K> ld{(const uint16_t *)tile8, RS, nw1, a.E};
+    sap_solve_mw<SANTA_NW, K>(n, ld, S, steps, fallbacks, exact);
   }
-  if (st != 0) {  // cannot happen for finite int64 costs; keep the contract
-    if (lane == 0) atomicOr(a.err, 2);
-    return;
-  }
-  __syncthreads();
   // -- outputs: col, exact cost, happiness deltas, apply ---------------------
   int64_t cost = 0, dch = 0, dgh = 0;
-  for (int i = lane; i < n; i += WAVE) {
-    const int col = c4r_l[i];
+  for (int i = tid; i < n; i += SANTA_WG) {
+    const int col = S.c4r[i];
     if (a.col) a.col[(size_t)b * n + i] = col;
     const int told = ctype[i], tnew = ctype[col];
     const int child = rows_l[i];
     if (MODE == 0) {
-      const uint32_t cn = tile8[(size_t)i * RS + slot_of(col, K)];
-      const uint32_t co = tile8[(size_t)i * RS + slot_of(i, K)];
+      const uint32_t cn = tile8[(size_t)i * RS + col];
+      const uint32_t co = tile8[(size_t)i * RS + i];
       cost += single_cost(cn, nw1, a.E);
       dch += child_happy(cn, nw1) - child_happy(co, nw1);
       dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
     } else {
       const uint16_t *t16 = (const uint16_t *)tile8;
-      const uint32_t cn = t16[(size_t)i * RS + slot_of(col, K)];
-      const uint32_t co = t16[(size_t)i * RS + slot_of(i, K)];
+      const uint32_t cn = t16[(size_t)i * RS + col];
+      const uint32_t co = t16[(size_t)i * RS + i];
       cost += twin_cost(cn, nw1, a.E);
       dch += child_happy(cn & 0xFF, nw1) + child_happy(cn >> 8, nw1) -
              child_happy(co & 0xFF, nw1) - child_happy(co >> 8, nw1);
@@ -465,92 +737,134 @@ __global__ __launch_bounds__(WAVE) void santa_block_kernel(SantaArgs a) {
   cost = wave_sum_i64(cost);
   dch = wave_sum_i64(dch);
   dgh = wave_sum_i64(dgh);
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) {
+    part[3 * w + 0] = cost;
+    part[3 * w + 1] = dch;
+    part[3 * w + 2] = dgh;
+  }
   // Apply: this block owns rows_l[*] (and rows_l[*]+1 for twins); it read
   // every old type into ctype before this point, so in-place is race-free.
-  for (int i = lane; i < n; i += WAVE) {
-    const int16_t tnew = ctype[c4r_l[i]];
+  for (int i = tid; i < n; i += SANTA_WG) {
+    const int16_t tnew = ctype[S.c4r[i]];
     a.types[rows_l[i]] = tnew;
     if (MODE) a.types[rows_l[i] + 1] = tnew;
   }
-  if (lane == 0) {
-    if (a.cost) a.cost[b] = cost;
+  __syncthreads();
+  if (tid == 0) {
+    int64_t tc = 0, td0 = 0, td1 = 0;
+    for (int q = 0; q < SANTA_NW; ++q) {
+      tc += part[3 * q];
+      td0 += part[3 * q + 1];
+      td1 += part[3 * q + 2];
+    }
+    if (a.cost) a.cost[b] = tc;
     if (a.steps) a.steps[b] = steps;
     if (a.delta) {
-      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
-      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
+      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)td0);
+      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)td1);
     }
+    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Generic batched LSAP: rows streamed from global memory (L2/MALL/HBM).
+// Generic batched LSAP.  int64 paths use the multi-wave solver (rows streamed
+// from global memory, or generated by hash); float64 uses the single-wave
+// scipy-replay solver sap_solve<K, double>.
 // ---------------------------------------------------------------------------
-template <int K, typename T, typename S>
-struct GlobalLoader {
-  const S *base;  // this block's n x n matrix
+template <int K, typename S>
+struct GlobalLoaderF64 {
+  const S *base;
   int n;
-  __device__ __forceinline__ void load(int i, T (&c)[K]) const {
+  __device__ __forceinline__ void load(int i, double (&c)[K]) const {
     const S *row = base + (size_t)i * n;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int j = threadIdx.x + WAVE * k;
-      c[k] = (j < n) ? (T)row[j] : (T)0;
+      c[k] = (j < n) ? (double)row[j] : 0.0;
     }
   }
 };
+
+template <int NW, int K, typename S, bool HASH>
+__global__ __launch_bounds__(NW * WAVE) void lsap_i64_kernel(const S *C, uint64_t seed, int64_t mod,
+                                                             int n, int32_t *col, int64_t *cost,
+                                                             int32_t *fb, unsigned flags) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  size_t off = 0;
+  SolveLds Sl;
+  Sl.u = (int64_t *)(smem + off);    off += r16((size_t)n * 8);
+  Sl.c4r = (int16_t *)(smem + off);  off += r16((size_t)n * 2);
+  Sl.r4c = (int16_t *)(smem + off);  off += r16((size_t)n * 2);
+  Sl.path = (int16_t *)(smem + off); off += r16((size_t)n * 2);
+  Sl.red = (uint64_t *)(smem + off); off += r16((size_t)4 * NW * 8);
+  int64_t *part = (int64_t *)(smem + off);
+  for (int i = tid; i < n; i += NW * WAVE) {
+    Sl.u[i] = 0;
+    Sl.c4r[i] = -1;
+    Sl.r4c[i] = -1;
+  }
+  __syncthreads();
+  int64_t steps = 0;
+  int fallbacks = 0;
+  const bool exact = (flags & SH_FLAG_EXACT_ARGMIN) != 0;
+  if constexpr (HASH) {
+    const HashLoader<NW, K> ld{seed, mod, (uint64_t)b, n};
+    sap_solve_mw<NW, K>(n, ld, Sl, steps, fallbacks, exact);
+  } else {
+    const GlobalLoader<NW, K, S> ld{C + (size_t)b * n * n, n};
+    sap_solve_mw<NW, K>(n, ld, Sl, steps, fallbacks, exact);
+  }
+  int64_t acc = 0;
+  for (int i = tid; i < n; i += NW * WAVE) {
+    const int cidx = Sl.c4r[i];
+    col[(size_t)b * n + i] = cidx;
+    if (cost) {
+      if constexpr (HASH)
+        acc += (int64_t)(sh_hash_cost(seed, (uint64_t)b, (uint64_t)i, (uint64_t)cidx) % (uint64_t)mod);
+      else
+        acc += (int64_t)C[(size_t)b * n * n + (size_t)i * n + cidx];
+    }
+  }
+  acc = wave_sum_i64(acc);
+  if ((tid & 63) == 0) part[tid >> 6] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    int64_t t = 0;
+    for (int q = 0; q < NW; ++q) t += part[q];
+    if (cost) cost[b] = t;
+    if (fallbacks && fb) atomicAdd(fb, fallbacks);
+  }
+}
 
 template <int K>
-struct HashLoader {
-  uint64_t seed;
-  int64_t mod;
-  uint64_t b;
-  int n;
-  __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int j = threadIdx.x + WAVE * k;
-      c[k] = (j < n) ? (int64_t)(sh_hash_cost(seed, b, (uint64_t)i, (uint64_t)j) % (uint64_t)mod)
-                     : 0;
-    }
-  }
-};
-
-template <int K, typename T, typename S, bool HASH>
-__global__ __launch_bounds__(WAVE) void lsap_kernel(const S *C, uint64_t seed, int64_t mod,
-                                                    int n, int32_t *col, T *cost) {
+__global__ __launch_bounds__(WAVE) void lsap_f64_kernel(const double *C, int n, int32_t *col,
+                                                        double *cost) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
-  T *u_l = (T *)smem;
-  int16_t *c4r_l = (int16_t *)(smem + r16((size_t)n * sizeof(T)));
+  double *u_l = (double *)smem;
+  int16_t *c4r_l = (int16_t *)(smem + r16((size_t)n * sizeof(double)));
   for (int i = lane; i < n; i += WAVE) {
     u_l[i] = 0;
     c4r_l[i] = -1;
   }
   __syncthreads();
   int64_t steps = 0;
-  int st;
-  if constexpr (HASH) {
-    HashLoader<K> ld{seed, mod, (uint64_t)b, n};
-    st = sap_solve<K, T>(n, ld, u_l, c4r_l, steps);
-  } else {
-    GlobalLoader<K, T, S> ld{C + (size_t)b * n * n, n};
-    st = sap_solve<K, T>(n, ld, u_l, c4r_l, steps);
-  }
+  GlobalLoaderF64<K, double> ld{C + (size_t)b * n * n, n};
+  const int st = sap_solve<K, double>(n, ld, u_l, c4r_l, steps);
   __syncthreads();
-  T acc = 0;
+  double acc = 0;
   for (int i = lane; i < n; i += WAVE) {
     const int cidx = (st == 0) ? c4r_l[i] : -1;
     col[(size_t)b * n + i] = cidx;
-    if (st == 0 && cost) {
-      if constexpr (HASH)
-        acc += (T)(sh_hash_cost(seed, (uint64_t)b, (uint64_t)i, (uint64_t)cidx) % (uint64_t)mod);
-      else
-        acc += (T)C[(size_t)b * n * n + (size_t)i * n + cidx];
-    }
+    if (st == 0 && cost) acc += C[(size_t)b * n * n + (size_t)i * n + cidx];
   }
   if (cost) {
-    // wave sum in lane order (deterministic); float64 order differs from numpy.
+    // wave sum in a fixed order (deterministic); it differs from numpy's sum
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, WAVE);
     if (lane == 0) cost[b] = acc;
@@ -846,16 +1160,15 @@ int sh_sample_blocks(uint64_t seed, uint64_t round, int lo, int count, int strid
 namespace {
 template <int K, int MODE>
 int launch_santa(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
-  const SantaLds L = santa_lds_layout(a.n, K, MODE, ctx->ng);
-  if (L.total > 160 * 1024)
-    return fail(SH_ERR_ARGS, "block too large for the LDS tile (n x 64K bytes)");
-  static thread_local bool attr_set = false;
-  if (!attr_set) {
+  const SantaLds L = santa_lds_layout(a.n, MODE, ctx->ng);
+  if (L.total > 160 * 1024) return fail(SH_ERR_ARGS, "block too large for the LDS tile");
+  static thread_local size_t attr_set = 0;
+  if (L.total > 64 * 1024 && L.total > attr_set) {
     HIP_TRY(hipFuncSetAttribute((const void *)santa_block_kernel<K, MODE>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total));
+    attr_set = L.total;
   }
-  hipLaunchKernelGGL((santa_block_kernel<K, MODE>), dim3(B), dim3(WAVE), L.total, s, a);
+  hipLaunchKernelGGL((santa_block_kernel<K, MODE>), dim3(B), dim3(SANTA_WG), L.total, s, a);
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
@@ -866,7 +1179,6 @@ extern "C" {
 int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, int16_t *d_types,
                     int32_t *d_col, int64_t *d_cost, int64_t *d_delta, int64_t *d_steps,
                     unsigned flags, void *stream) {
-  (void)flags;
   if (!ctx || !d_rows || !d_types) return fail(SH_ERR_ARGS, "null pointer");
   if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS) return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > 256) return fail(SH_ERR_ARGS, "n must be in [1, 256] for the LDS-tile path");
@@ -876,21 +1188,18 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   a.rows = d_rows; a.types = d_types; a.col = d_col; a.cost = d_cost; a.delta = d_delta;
   a.steps = d_steps; a.wish = ctx->d_wish; a.csr_off = ctx->d_csr_off; a.csr = ctx->d_csr;
   a.err = ctx->d_err; a.E = ctx->E; a.n = n; a.nc = ctx->nc; a.ng = ctx->ng;
-  a.n_wish = ctx->n_wish; a.n_good = ctx->n_good;
+  a.n_wish = ctx->n_wish; a.n_good = ctx->n_good; a.flags = flags;
   hipStream_t s = (hipStream_t)stream;
-  const int K = pick_k(n);
-  if (mode == SH_MODE_SINGLE) {
-    switch (K) {
-      case 1: return launch_santa<1, 0>(ctx, a, B, s);
-      case 2: return launch_santa<2, 0>(ctx, a, B, s);
-      default: return launch_santa<4, 0>(ctx, a, B, s);
-    }
-  }
-  switch (K) {
-    case 1: return launch_santa<1, 1>(ctx, a, B, s);
-    case 2: return launch_santa<2, 1>(ctx, a, B, s);
-    default: return launch_santa<4, 1>(ctx, a, B, s);
-  }
+  return mode == SH_MODE_SINGLE ? launch_santa<1, 0>(ctx, a, B, s) : launch_santa<1, 1>(ctx, a, B, s);
+}
+
+int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream) {
+  if (!ctx) return fail(SH_ERR_ARGS, "null ctx");
+  int32_t h = 0;
+  HIP_TRY(hipMemcpyAsync(&h, ctx->d_err + 1, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  HIP_TRY(hipMemsetAsync(ctx->d_err + 1, 0, 4, (hipStream_t)stream));
+  return h;
 }
 
 int sh_score(sh_ctx *ctx, const int16_t *d_types, int64_t *d_sums, void *stream) {
@@ -933,19 +1242,38 @@ int sh_unpack_types(int16_t *d_types, const int32_t *d_rows, int count, const in
 }  // extern "C"
 
 namespace {
-template <typename T, typename S, bool HASH>
-int launch_lsap(const S *C, uint64_t seed, int64_t mod, int n, int B, int32_t *col, T *cost,
-                hipStream_t s) {
+int check_lsap_args(int n, int B, const int32_t *col) {
   if (n <= 0 || n > SH_MAX_N) return fail(SH_ERR_ARGS, "n must be in [1, 1024]");
   if (B < 0) return fail(SH_ERR_ARGS, "B < 0");
   if (!col) return fail(SH_ERR_ARGS, "null col");
-  if (B == 0) return SH_OK;
-  const size_t lds = r16((size_t)n * sizeof(T)) + r16((size_t)n * 2);
-  const int K = pick_k(n);
-#define L_(KK)                                                                          \
-  hipLaunchKernelGGL((lsap_kernel<KK, T, S, HASH>), dim3(B), dim3(WAVE), lds, s, C, seed, \
-                     mod, n, col, cost)
-  switch (K) {
+  return SH_OK;
+}
+
+template <typename S, bool HASH>
+int launch_lsap_i64(const S *C, uint64_t seed, int64_t mod, int n, int B, int32_t *col,
+                    int64_t *cost, unsigned flags, hipStream_t s) {
+  const int rc = check_lsap_args(n, B, col);
+  if (rc || B == 0) return rc;
+  const int NW = n <= WAVE ? 1 : 4;
+  const size_t lds = r16((size_t)n * 8) + 3 * r16((size_t)n * 2) + r16((size_t)4 * NW * 8) + 64;
+#define L_(NWW, KK)                                                                            \
+  hipLaunchKernelGGL((lsap_i64_kernel<NWW, KK, S, HASH>), dim3(B), dim3(NWW * WAVE), lds, s, C, \
+                     seed, mod, n, col, cost, (int32_t *)nullptr, flags)
+  if (NW == 1) L_(1, 1);
+  else if (n <= 256) L_(4, 1);
+  else if (n <= 512) L_(4, 2);
+  else L_(4, 4);
+#undef L_
+  HIP_TRY(hipGetLastError());
+  return SH_OK;
+}
+
+int launch_lsap_f64(const double *C, int n, int B, int32_t *col, double *cost, hipStream_t s) {
+  const int rc = check_lsap_args(n, B, col);
+  if (rc || B == 0) return rc;
+  const size_t lds = r16((size_t)n * 8) + r16((size_t)n * 2);
+#define L_(KK) hipLaunchKernelGGL((lsap_f64_kernel<KK>), dim3(B), dim3(WAVE), lds, s, C, n, col, cost)
+  switch (pick_k(n)) {
     case 1: L_(1); break;
     case 2: L_(2); break;
     case 4: L_(4); break;
@@ -962,31 +1290,28 @@ extern "C" {
 
 int lsap_solve_batched_i64(const int64_t *d_C, int n, int B, int32_t *d_col, int64_t *d_cost,
                            unsigned flags, void *stream) {
-  (void)flags;
   if (!d_C) return fail(SH_ERR_ARGS, "null C");
-  return launch_lsap<int64_t, int64_t, false>(d_C, 0, 1, n, B, d_col, d_cost, (hipStream_t)stream);
+  return launch_lsap_i64<int64_t, false>(d_C, 0, 1, n, B, d_col, d_cost, flags, (hipStream_t)stream);
 }
 
 int lsap_solve_batched_i32(const int32_t *d_C, int n, int B, int32_t *d_col, int64_t *d_cost,
                            unsigned flags, void *stream) {
-  (void)flags;
   if (!d_C) return fail(SH_ERR_ARGS, "null C");
-  return launch_lsap<int64_t, int32_t, false>(d_C, 0, 1, n, B, d_col, d_cost, (hipStream_t)stream);
+  return launch_lsap_i64<int32_t, false>(d_C, 0, 1, n, B, d_col, d_cost, flags, (hipStream_t)stream);
 }
 
 int lsap_solve_batched_f64(const double *d_C, int n, int B, int32_t *d_col, double *d_cost,
                            unsigned flags, void *stream) {
-  (void)flags;
   if (!d_C) return fail(SH_ERR_ARGS, "null C");
-  return launch_lsap<double, double, false>(d_C, 0, 1, n, B, d_col, d_cost, (hipStream_t)stream);
+  (void)flags;
+  return launch_lsap_f64(d_C, n, B, d_col, d_cost, (hipStream_t)stream);
 }
 
 int lsap_solve_batched_hash(uint64_t seed, int64_t modulus, int n, int B, int32_t *d_col,
                             int64_t *d_cost, unsigned flags, void *stream) {
-  (void)flags;
   if (modulus <= 0) return fail(SH_ERR_ARGS, "modulus must be > 0");
-  return launch_lsap<int64_t, int64_t, true>(nullptr, seed, modulus, n, B, d_col, d_cost,
-                                             (hipStream_t)stream);
+  return launch_lsap_i64<int64_t, true>(nullptr, seed, modulus, n, B, d_col, d_cost, flags,
+                                        (hipStream_t)stream);
 }
 
 }  // extern "C"

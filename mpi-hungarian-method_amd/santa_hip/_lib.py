@@ -19,6 +19,8 @@ SH_ERR_HIP = -3
 SH_MODE_SINGLE = 0
 SH_MODE_TWINS = 1
 SH_COMPAT_TIEBREAK = 1
+SH_FLAG_EXACT_ARGMIN = 2
+SH_FLAG_BUILD_ONLY = 4
 SH_MAX_N = 1024
 SH_MAX_N_SANTA = 256
 
@@ -38,6 +40,7 @@ SIGNATURES = {
     "sh_solve_blocks": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _U, _P]),
     "sh_score": (_I, [_P, _P, _P, _P]),
     "sh_ctx_error_flags": (_I, [_P, _P]),
+    "sh_ctx_fallback_steps": (_I, [_P, _P]),
     "sh_pack_types": (_I, [_P, _P, _I, _P, _P]),
     "sh_unpack_types": (_I, [_P, _P, _I, _P, _I, _P]),
     "lsap_solve_batched_i64": (_I, [_P, _I, _I, _P, _P, _U, _P]),

@@ -105,7 +105,8 @@ class SantaGPU:
     # -- A2-A6 fused block round ----------------------------------------------------
     def solve_blocks(self, mode: int, rows: torch.Tensor, n: int, types: torch.Tensor,
                      col: torch.Tensor | None = None, cost: torch.Tensor | None = None,
-                     delta: torch.Tensor | None = None, steps: torch.Tensor | None = None) -> None:
+                     delta: torch.Tensor | None = None, steps: torch.Tensor | None = None,
+                     flags: int = 0) -> None:
         """Build, solve and apply B = rows.numel() // n disjoint blocks in place."""
         assert rows.dtype == torch.int32 and rows.is_contiguous() and rows.device == self.device
         assert types.dtype == torch.int16 and types.numel() == self.nc and types.device == self.device
@@ -117,11 +118,16 @@ class SantaGPU:
                 assert t.dtype == dt and t.numel() >= size and t.device == self.device
         rc = _lib.lib().sh_solve_blocks(self._h, mode, _ptr(rows), n, B, _ptr(types), _ptr(col),
                                         _ptr(cost), _ptr(delta), _ptr(steps),
-                                        _lib.SH_COMPAT_TIEBREAK, self.stream)
+                                        _lib.SH_COMPAT_TIEBREAK | flags, self.stream)
         _lib.check(rc, "sh_solve_blocks")
 
     def error_flags(self) -> int:
         return _lib.check(_lib.lib().sh_ctx_error_flags(self._h, self.stream), "sh_ctx_error_flags")
+
+    def fallback_steps(self) -> int:
+        """Steps since the last call that used the exact two-pass argmin."""
+        return _lib.check(_lib.lib().sh_ctx_fallback_steps(self._h, self.stream),
+                          "sh_ctx_fallback_steps")
 
     # -- A7 score ---------------------------------------------------------------
     def score_sums_async(self, types: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:

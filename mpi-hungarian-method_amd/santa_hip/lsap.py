@@ -23,10 +23,14 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-def solve_batched(C: torch.Tensor, with_cost: bool = True):
+INT64_COST_LIMIT = 1 << 50  # |C| bound that keeps every SAP value < 2^62 (n <= 1024)
+
+
+def solve_batched(C: torch.Tensor, with_cost: bool = True, flags: int = 0):
     """C: device tensor [B, n, n] (int64 / int32 / float64) -> (col int32 [B, n], cost [B]).
 
-    Infeasible blocks get col = -1 (float64 with +inf only)."""
+    Infeasible blocks get col = -1 (float64 with +inf only).  int64 costs
+    must satisfy |C| < 2^50 (checked on the device)."""
     require_gpu()
     if C.dim() != 3 or C.shape[1] != C.shape[2]:
         raise ValueError("expected [B, n, n]")
@@ -36,15 +40,18 @@ def solve_batched(C: torch.Tensor, with_cost: bool = True):
     col = torch.empty((B, n), dtype=torch.int32, device=dev)
     s = current_stream_handle(dev)
     L = _lib.lib()
+    fl = _lib.SH_COMPAT_TIEBREAK | flags
     if C.dtype == torch.int64:
+        if C.numel() and int(C.abs().max()) >= INT64_COST_LIMIT:
+            raise ValueError("int64 costs must satisfy |C| < 2**50; pass float64 instead")
         cost = torch.empty(B, dtype=torch.int64, device=dev) if with_cost else None
-        rc = L.lsap_solve_batched_i64(_p(C), n, B, _p(col), _p(cost), _lib.SH_COMPAT_TIEBREAK, s)
+        rc = L.lsap_solve_batched_i64(_p(C), n, B, _p(col), _p(cost), fl, s)
     elif C.dtype == torch.int32:
         cost = torch.empty(B, dtype=torch.int64, device=dev) if with_cost else None
-        rc = L.lsap_solve_batched_i32(_p(C), n, B, _p(col), _p(cost), _lib.SH_COMPAT_TIEBREAK, s)
+        rc = L.lsap_solve_batched_i32(_p(C), n, B, _p(col), _p(cost), fl, s)
     elif C.dtype == torch.float64:
         cost = torch.empty(B, dtype=torch.float64, device=dev) if with_cost else None
-        rc = L.lsap_solve_batched_f64(_p(C), n, B, _p(col), _p(cost), _lib.SH_COMPAT_TIEBREAK, s)
+        rc = L.lsap_solve_batched_f64(_p(C), n, B, _p(col), _p(cost), fl, s)
     else:
         raise TypeError(f"unsupported dtype {C.dtype}")
     _lib.check(rc, "lsap_solve_batched")
@@ -83,7 +90,8 @@ def linear_sum_assignment(cost_matrix, maximize: bool = False, device: int | str
     if maximize:
         C = -C
     dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
-    if np.issubdtype(C.dtype, np.integer) or C.dtype == np.bool_:
+    if (np.issubdtype(C.dtype, np.integer) or C.dtype == np.bool_) and \
+            (C.size == 0 or int(np.abs(C.astype(np.int64)).max()) < INT64_COST_LIMIT):
         Ct = torch.from_numpy(np.ascontiguousarray(C, dtype=np.int64)).to(dev)
     else:
         Cf = np.ascontiguousarray(C, dtype=np.float64)

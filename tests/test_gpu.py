@@ -263,3 +263,44 @@ def test_pack_unpack_roundtrip(sh, ctx, full_data):
     r = rows.cpu().numpy()
     t2n = t2.cpu().numpy()
     assert np.array_equal(t2n[r], full_data.types[r]) and np.array_equal(t2n[r + 1], full_data.types[r])
+
+
+# --------------------------------------------------------------------------- argmin paths
+def test_fast_and_exact_argmin_agree(sh, ctx, full_data):
+    """The packed-key DPP argmin and the two-pass exact argmin (forced by
+    SH_FLAG_EXACT_ARGMIN) make identical decisions."""
+    from santa_hip import _lib
+    for mode, n, B in ((0, 256, 32), (1, 256, 4)):
+        rows = ctx.sample_blocks(mode, n, B, 31, 2)
+        outs = []
+        for fl in (0, _lib.SH_FLAG_EXACT_ARGMIN):
+            types = ctx.upload_types(full_data.types)
+            col = torch.empty(B * n, dtype=torch.int32, device="cuda")
+            ctx.solve_blocks(mode, rows, n, types, col=col, flags=fl)
+            outs.append((col.cpu().numpy(), types.cpu().numpy()))
+        assert np.array_equal(outs[0][0], outs[1][0])
+        assert np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_lsap_wide_range_int64_uses_exact_fallback(sh):
+    """Spreads beyond the packed key's 2^52 window take the exact argmin."""
+    rng = np.random.default_rng(11)
+    C = rng.integers(-(1 << 49), 1 << 49, size=(3, 128, 128), dtype=np.int64)
+    col, cost = sh.solve_batched(torch.from_numpy(C).cuda())
+    ocol, ocost = oracle.lsap_i64_batched(C)
+    assert np.array_equal(col.cpu().numpy(), ocol)
+    assert np.array_equal(cost.cpu().numpy(), ocost)
+    with pytest.raises(ValueError):
+        sh.solve_batched(torch.from_numpy(C * 4).cuda())
+
+
+def test_no_fallback_on_santa_rounds(sh, ctx, full_data):
+    """Santa cost spreads stay inside the packed key's window: the exact
+    two-pass argmin is never needed on real rounds (performance guard)."""
+    ctx.fallback_steps()
+    types = ctx.upload_types(full_data.types)
+    for mode, n in ((0, 256), (1, 256)):
+        _, _, _, nb = ctx.geometry(mode, n)
+        rows = ctx.sample_blocks(mode, n, min(nb, 512), 5, 0)
+        ctx.solve_blocks(mode, rows, n, types)
+    assert ctx.fallback_steps() == 0
