@@ -1,0 +1,93 @@
+"""Multi-rank driver logic on the CPU (gloo, world_size 2 and 3).
+
+The product exchange (santa_hip.driver.exchange: shard -> pack -> one
+all-gather -> unpack) and round loop run with the oracle-backed CPU engine;
+the final assignment and every per-round score must equal the single-rank
+run bit for bit (blocks are disjoint, integer sums are order-free), including
+block counts that do not divide evenly across ranks and the twins rollback."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from santa_hip import _lib
+from santa_hip import data as D
+from santa_hip.driver import World, run_rounds, shard_range
+
+SMALL = dict(seed=3, nc=60000, ng=60, nq=1000, n_wish=20, n_good=300)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(eng_data, mode, n, bpr, rounds, world=None):
+    from cpu_engine import CPUOracleEngine
+    sd = eng_data
+    eng = CPUOracleEngine(sd.wish, sd.goodkids, sd.nq)
+    types = torch.from_numpy(sd.types.copy())
+    res = run_rounds(eng, types, mode=mode, n=n, blocks_per_round=bpr, seed=17,
+                     max_rounds=rounds, world=world or World(), patience=100)
+    return types.numpy().copy(), [st.score for st in res.history]
+
+
+def _worker(rank, size, port, mode, n, bpr, rounds, out):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    for p in (os.path.join(root, "mpi-hungarian-method_amd"), os.path.join(root, "oracle"), here):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    sd = D.synthetic(**SMALL)
+    t, scores = _run(sd, mode, n, bpr, rounds, World(rank, size, None))
+    out[rank] = (t, scores)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("size,mode,n,bpr", [(2, 0, 64, None), (3, 0, 100, 7), (2, 1, 16, None)])
+def test_multirank_equals_single_rank(size, mode, n, bpr):
+    sd = D.synthetic(**SMALL)
+    rounds = 3
+    ref_t, ref_scores = _run(sd, mode, n, bpr, rounds)
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(size, port, mode, n, bpr, rounds, out), nprocs=size, join=True)
+    for r in range(size):
+        t, scores = out[r]
+        assert np.array_equal(t, ref_t), f"rank {r} state differs"
+        assert scores == ref_scores
+
+
+def test_shard_range_covers_blocks():
+    for B in (1, 7, 78, 3730):
+        for size in (1, 2, 3, 4, 8):
+            seen = []
+            for r in range(size):
+                b0, b1, per = shard_range(B, r, size)
+                assert b1 - b0 <= per
+                seen.extend(range(b0, b1))
+            assert seen == list(range(B))
+
+
+def test_twins_rank_limit_matches_reference():
+    """mpi_twins.py:128,132 raises IndexError with more ranks than twin
+    blocks; the reference-schedule driver refuses that configuration."""
+    from cpu_engine import CPUOracleEngine
+    sd = D.synthetic(**SMALL)
+    eng = CPUOracleEngine(sd.wish, sd.goodkids, sd.nq)
+    _, _, _, nb = eng.geometry(_lib.SH_MODE_TWINS, 64)
+    with pytest.raises(ValueError):
+        run_rounds(eng, torch.from_numpy(sd.types.copy()), mode=_lib.SH_MODE_TWINS, n=64,
+                   blocks_per_round=1, world=World(0, nb + 1, None), max_rounds=1)
