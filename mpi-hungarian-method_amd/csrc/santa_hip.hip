@@ -305,6 +305,40 @@ __device__ __forceinline__ uint64_t wave_min_u64_dpp(uint64_t x) {
   return readlane_u64(x, 63);
 }
 
+// 32-bit unsigned min over the wave with the DPP modifier fused into
+// v_min_u32 (one instruction per level); the result is read from lane 63.
+// Hazards are explicit: a VALU write followed by a DPP read of the same VGPR
+// needs two wait states (s_nop 1) on GFX9.
+__device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t x) {
+  uint32_t r;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_readlane_b32 %1, %0, 63"
+      : "+v"(x), "=s"(r));
+  return r;
+}
+
+// 64-bit unsigned min as two fused 32-bit reductions (high word, then the
+// low word among the lanes holding the minimal high word).
+__device__ __forceinline__ uint64_t wave_min_u64_fast(uint64_t x) {
+  const uint32_t h = (uint32_t)(x >> 32);
+  const uint32_t mh = wave_min_u32_dpp(h);
+  const uint32_t ml = wave_min_u32_dpp(h == mh ? (uint32_t)x : 0xFFFFFFFFu);
+  return ((uint64_t)mh << 32) | ml;
+}
+
 constexpr int KEY_LO_BITS = 21;
 constexpr uint64_t KEY_HI_MAX = (1ull << 43) - 1;
 constexpr int64_t KEY_BIAS = 1ll << 42;
@@ -387,7 +421,9 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
         const uint64_t key = (key_hi_of((uint64_t)spc[k] + kb) << KEY_LO_BITS) | lo;
         best = umin64(best, act ? key : ~0ull);
       }
-      uint64_t g = block_min_u64<NW>(wave_min_u64_dpp(best), S.red + par * NW, w);
+      uint64_t g = block_min_u64<NW>(wave_min_u64_fast(best), S.red + par * NW, w);
+      g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
+          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
       par ^= 1;
       const uint64_t hi = g >> KEY_LO_BITS;
       if (exact || hi == 0 || hi == KEY_HI_MAX) {

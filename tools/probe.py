@@ -1,0 +1,54 @@
+"""Kernel probe: times the fused block kernel's phases on round 0 of the
+benchmark workload (build only vs build+solve), with HIP events.  Used with
+rocprofv3 --pmc to attribute per-step cycles.  Not part of the product."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpi-hungarian-method_amd"))
+import torch  # noqa: E402
+
+from santa_hip import _lib, data as D  # noqa: E402
+from santa_hip.context import SantaGPU  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--n", type=int, default=256)
+    ap.add_argument("--blocks", type=int, default=0, help="0 = full round")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--phase", choices=["all", "build", "solve"], default="all")
+    a = ap.parse_args()
+    sd = D.synthetic(2017)
+    ctx = SantaGPU.from_data(sd, 0)
+    _, _, _, nb = ctx.geometry(a.mode, a.n)
+    B = a.blocks or nb
+    rows = ctx.sample_blocks(a.mode, a.n, B, 2017, 0)
+    base = ctx.upload_types(sd.types)
+    steps = torch.empty(B, dtype=torch.int64, device="cuda")
+    out = {}
+    for name, fl in (("build", _lib.SH_FLAG_BUILD_ONLY), ("solve", 0)):
+        if a.phase not in ("all", name):
+            continue
+        ts = []
+        for _ in range(a.reps):
+            t = base.clone()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ctx.solve_blocks(a.mode, rows, a.n, t, steps=steps, flags=fl)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        out[name] = {"ms": min(ts), "all_ms": ts}
+    out["blocks"] = B
+    out["steps_total"] = int(steps.sum())
+    out["steps_per_block"] = int(steps.sum()) / B
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
