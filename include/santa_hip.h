@@ -45,6 +45,8 @@ extern "C" {
 #define SH_FLAG_EXACT_ARGMIN 2u /* always use the two-pass exact argmin    */
 #define SH_FLAG_BUILD_ONLY 4u   /* sh_solve_blocks: build the cost tiles and
                                    apply the identity (phase timing only)  */
+#define SH_FLAG_LDS_TILE 8u     /* sh_solve_blocks: previous kernel design
+                                   (cost tile in LDS), for A/B profiling   */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024

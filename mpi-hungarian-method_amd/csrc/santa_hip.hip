@@ -805,6 +805,417 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Register-tile Santa kernel (n <= 256, the production path).
+//
+// Same algorithm and decisions as santa_block_kernel + sap_solve_mw, laid
+// out so that a Dijkstra step touches LDS only for the 4-partial argmin:
+//  * thread j owns column j and keeps the column of the rank-code tile in
+//    VGPRs (singles: 256 uint8 codes = 64 dwords; twins: 256 uint16 = 128),
+//    read with a wave-uniform row index through s_set_gpr_idx (no scratch);
+//  * every wave keeps its own copy of the row duals, row r in lane r&63,
+//    slot r>>6.  The copies change only through wave-uniform facts (each
+//    step's winner), so the four copies stay identical without messages:
+//    when row i is reached at the step whose new minimum is m, u~[i] -= m;
+//    at the end of the Dijkstra every visited row gets += the final minimum.
+//    Then the relaxation of a visited row needs no minVal term:
+//    r = C[i][j] - u~[i] - v[j]  (the -m cancels scipy's minVal + ...).
+//  * the tile is built through an 8 KB LDS stage, 32 rows (16 pairs) at a
+//    time, with the next group's wishlist loads in flight.
+// LDS ~16 KB per block, so residency is set by VGPRs: 4 singles blocks per
+// CU (16 waves) instead of 2 with the 64 KB LDS tile.
+// ---------------------------------------------------------------------------
+typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int MODE> struct RegTile;
+
+template <> struct RegTile<0> {  // uint8 codes, 4 rows per dword
+  static constexpr int DW = 64;  // dwords per column
+  static constexpr int ROWS_PER_DW = 4;
+  u32x32 a, b;
+  __device__ __forceinline__ void set(int q, uint32_t w) {
+    if (q < 32) a[q] = w; else b[q - 32] = w;
+  }
+  __device__ __forceinline__ uint32_t get(int i) const {  // i wave-uniform
+    const int d = i >> 2;
+    uint32_t w0 = a[d & 31], w1 = b[d & 31];
+    asm volatile("" : "+v"(w0));
+    asm volatile("" : "+v"(w1));
+    const uint32_t w = (d < 32) ? w0 : w1;
+    return (w >> (8 * (i & 3))) & 0xFFu;
+  }
+};
+
+template <> struct RegTile<1> {  // uint16 code pairs, 2 rows per dword
+  [[maybe_unused]] static constexpr int DW = 128;
+  [[maybe_unused]] static constexpr int ROWS_PER_DW = 2;
+  // (not instantiated by the launcher: the four 32-dword tuples are spilled
+  //  by the register allocator, so twins use the LDS-tile kernel)
+  u32x32 a, b, c, d;
+  __device__ __forceinline__ void set(int q, uint32_t w) {
+    if (q < 32) a[q] = w;
+    else if (q < 64) b[q - 32] = w;
+    else if (q < 96) c[q - 64] = w;
+    else d[q - 96] = w;
+  }
+  __device__ __forceinline__ uint32_t get(int i) const {
+    const int dw = i >> 1, x = dw & 31, q = dw >> 5;
+    uint32_t w0 = a[x], w1 = b[x], w2 = c[x], w3 = d[x];
+    asm volatile("" : "+v"(w0));
+    asm volatile("" : "+v"(w1));
+    asm volatile("" : "+v"(w2));
+    asm volatile("" : "+v"(w3));
+    const uint32_t w = (q == 0) ? w0 : (q == 1) ? w1 : (q == 2) ? w2 : w3;
+    return (w >> (16 * (i & 1))) & 0xFFFFu;
+  }
+};
+
+// A wave's private copy of the row duals: row r in lane r&63, slot r>>6.
+struct RowDuals {
+  u32x4 lo, hi;
+  __device__ __forceinline__ int64_t read(int r) const {  // r wave-uniform
+    uint32_t l = lo[r >> 6], h = hi[r >> 6];
+    asm volatile("" : "+v"(l));
+    asm volatile("" : "+v"(h));
+    const uint32_t L = (uint32_t)__builtin_amdgcn_readlane((int)l, r & 63);
+    const uint32_t H = (uint32_t)__builtin_amdgcn_readlane((int)h, r & 63);
+    return (int64_t)(((uint64_t)H << 32) | L);
+  }
+  __device__ __forceinline__ void add_owner(int r, int64_t d) {  // u[r] += d, r uniform
+    if ((int)(threadIdx.x & 63) == (r & 63)) {
+      const int k = r >> 6;
+      const uint64_t v = (((uint64_t)hi[k] << 32) | lo[k]) + (uint64_t)d;
+      lo[k] = (uint32_t)v;
+      hi[k] = (uint32_t)(v >> 32);
+    }
+  }
+};
+
+constexpr int VT_NW = 4;
+constexpr int VT_WG = VT_NW * WAVE;
+constexpr int VT_GROUP = 32;  // virtual rows (children) staged per group
+
+struct VtLds {
+  size_t stage, rows, ctype, head, nxt, c4r, r4c, path, red, part, total;
+};
+
+__host__ __device__ __forceinline__ VtLds vt_lds_layout(int ng) {
+  VtLds L;
+  size_t off = 0;
+  L.stage = off; off += (size_t)VT_GROUP * 256;  // 32 rows x 256 B, or 16 pairs x 256 x 2 B
+  L.rows = off;  off += 256 * 4;
+  L.ctype = off; off += 256 * 2;
+  L.head = off;  off += r16((size_t)ng * 4);
+  L.nxt = off;   off += 256 * 2;
+  L.c4r = off;   off += 256 * 2;
+  L.r4c = off;   off += 256 * 2;
+  L.path = off;  off += 256 * 2;
+  L.red = off;   off += 4 * VT_NW * 8;
+  L.part = off;  off += r16(VT_NW * 3 * 8);
+  L.total = off;
+  return L;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(SantaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = a.n;
+  const VtLds L = vt_lds_layout(a.ng);
+  uint8_t *stage = smem + L.stage;
+  int32_t *rows_l = (int32_t *)(smem + L.rows);
+  int16_t *ctype = (int16_t *)(smem + L.ctype);
+  int32_t *head = (int32_t *)(smem + L.head);
+  int16_t *nxt = (int16_t *)(smem + L.nxt);
+  int16_t *c4r_l = (int16_t *)(smem + L.c4r);
+  int16_t *r4c_l = (int16_t *)(smem + L.r4c);
+  int16_t *path_l = (int16_t *)(smem + L.path);
+  uint64_t *red = (uint64_t *)(smem + L.red);
+  int64_t *part = (int64_t *)(smem + L.part);
+
+  // -- rows, range check, chains ------------------------------------------------
+  int bad = 0;
+  if (tid < n) {
+    const int r = a.rows[(size_t)b * n + tid];
+    bad = (r < 0) || (r + MODE >= a.nc);
+    rows_l[tid] = r;
+  }
+  if (__syncthreads_or(bad)) {
+    if (tid == 0) atomicOr(a.err, 1);
+    return;
+  }
+  for (int t = tid; t < a.ng; t += VT_WG) head[t] = -1;
+  __syncthreads();
+  const int j = tid;  // this thread's column
+  int16_t my_type = -1;
+  if (j < n) {
+    my_type = a.types[rows_l[j]];
+    nxt[j] = (int16_t)atomicExch(&head[my_type], j);
+    ctype[j] = my_type;
+    c4r_l[j] = -1;
+    r4c_l[j] = -1;
+  }
+  __syncthreads();
+
+  // -- build the register tile, one 8 KB LDS stage group at a time ---------------
+  RegTile<MODE> T;
+  {
+    const int nw = a.n_wish;
+    const int vrows = n * (MODE ? 2 : 1);
+    const int ngroups = (vrows + VT_GROUP - 1) / VT_GROUP;
+    const bool vec = (nw & 3) == 0;
+    const int cpr = vec ? (nw >> 2) : nw;      // load units per virtual row
+    const int per_group = VT_GROUP * cpr;       // load units per group
+    constexpr int U = 4;                        // units per thread per group (cpr <= 32)
+    int uq[U], ur[U];                           // (row-in-group, unit) of tid + 256u
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = tid + VT_WG * u;
+      uq[u] = c / cpr;
+      ur[u] = c - uq[u] * cpr;
+    }
+    auto load_group = [&](int g, uint2 (&q)[U]) {
+      if (!vec) return;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int vr = g * VT_GROUP + uq[u];
+        if (tid + VT_WG * u < per_group && vr < vrows) {
+          const int child = rows_l[MODE ? (vr >> 1) : vr] + (MODE ? (vr & 1) : 0);
+          q[u] = *(const uint2 *)(a.wish + (size_t)child * nw + 4 * ur[u]);
+        }
+      }
+    };
+    auto put = [&](int lr, int r, int gift) {
+      for (int jj = head[gift]; jj >= 0; jj = nxt[jj]) {
+        if (MODE)  // stage[pair][col] as uint16, byte = twin
+          stage[((lr >> 1) * 256 + jj) * 2 + (lr & 1)] = (uint8_t)(r + 1);
+        else
+          stage[lr * 256 + jj] = (uint8_t)(r + 1);
+      }
+    };
+    uint2 cur[U], nxt_q[U];
+    load_group(0, cur);
+#pragma unroll
+    for (int g = 0; g < 256 * (MODE ? 2 : 1) / VT_GROUP; ++g) {
+      if (g < ngroups) {
+        if (g + 1 < ngroups) load_group(g + 1, nxt_q);
+        // zero the stage (8 KB: 32 B per thread)
+        ((uint4 *)stage)[2 * tid] = make_uint4(0, 0, 0, 0);
+        ((uint4 *)stage)[2 * tid + 1] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        if (vec) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int vr = g * VT_GROUP + uq[u];
+            if (tid + VT_WG * u < per_group && vr < vrows) {
+              const int lr = uq[u];  // virtual row within the group
+              const int r0 = 4 * ur[u];
+              put(lr, r0 + 0, (int16_t)(cur[u].x & 0xFFFFu));
+              put(lr, r0 + 1, (int16_t)(cur[u].x >> 16));
+              put(lr, r0 + 2, (int16_t)(cur[u].y & 0xFFFFu));
+              put(lr, r0 + 3, (int16_t)(cur[u].y >> 16));
+            }
+          }
+        } else {
+          for (int c = tid; c < per_group; c += VT_WG) {
+            const int lr = c / nw, r = c - lr * nw;
+            const int vr = g * VT_GROUP + lr;
+            if (vr < vrows) {
+              const int child = rows_l[MODE ? (vr >> 1) : vr] + (MODE ? (vr & 1) : 0);
+              put(lr, r, a.wish[(size_t)child * nw + r]);
+            }
+          }
+        }
+        __syncthreads();
+        // this thread's column for the group's 32 rows (16 pairs) -> 8 dwords
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          uint32_t dw;
+          if (MODE) {
+            const uint16_t *s16 = (const uint16_t *)stage;
+            dw = (uint32_t)s16[(2 * q) * 256 + j] | ((uint32_t)s16[(2 * q + 1) * 256 + j] << 16);
+          } else {
+            dw = (uint32_t)stage[(4 * q) * 256 + j] | ((uint32_t)stage[(4 * q + 1) * 256 + j] << 8) |
+                 ((uint32_t)stage[(4 * q + 2) * 256 + j] << 16) |
+                 ((uint32_t)stage[(4 * q + 3) * 256 + j] << 24);
+          }
+          T.set(8 * g + q, dw);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = nxt_q[u];
+      }
+    }
+  }
+
+  // -- solve ------------------------------------------------------------------------
+  const int nw1 = a.n_wish + 1;
+  const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
+  const int64_t INF = INT64_MAX;
+  const bool live = j < n;
+  int64_t spc = INF, nv = 0;
+  int path = -1, pos = -1, r4c = -1;
+  RowDuals U;
+  U.lo = u32x4{0, 0, 0, 0};
+  U.hi = u32x4{0, 0, 0, 0};
+  int64_t steps = 0;
+  int fallbacks = 0;
+  int par = 0;
+  if (a.flags & SH_FLAG_BUILD_ONLY) {
+    if (live) c4r_l[j] = (int16_t)j, r4c_l[j] = (int16_t)j;
+    __syncthreads();
+  } else {
+    for (int cur = 0; cur < n; ++cur) {
+      spc = INF;
+      pos = live ? (n - 1 - j) : -1;
+      r4c = live ? r4c_l[j] : -1;
+      uint32_t vis = ((cur & 63) == lane) ? (1u << (cur >> 6)) : 0u;
+      int nrem = n;
+      int64_t minVal = 0;
+      int i = cur;
+      int sink;
+      for (;;) {
+        ++steps;
+        const uint32_t code = T.get(i);
+        const int64_t c = MODE ? twin_cost(code, nw1, a.E) : single_cost(code, nw1, a.E);
+        const int64_t r = c + nv - U.read(i);
+        const bool act = pos >= 0;
+        const bool upd = act && (r < spc);
+        spc = upd ? r : spc;
+        path = upd ? i : path;
+        const uint64_t kb = (uint64_t)KEY_BIAS - (uint64_t)minVal;
+        const uint32_t lo = (r4c < 0) ? (((uint32_t)(1023 - pos) << 10) | (uint32_t)j)
+                                      : ((1u << 20) | ((uint32_t)pos << 10) | (uint32_t)r4c);
+        const uint64_t key = act ? ((key_hi_of((uint64_t)spc + kb) << KEY_LO_BITS) | lo) : ~0ull;
+        uint64_t g = block_min_u64<VT_NW>(wave_min_u64_fast(key), red + par * VT_NW, w);
+        g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+        par ^= 1;
+        const uint64_t hi = g >> KEY_LO_BITS;
+        if (exact || hi == 0 || hi == KEY_HI_MAX) {
+          uint64_t m = act ? ((uint64_t)spc ^ SIGN64) : ~0ull;
+          m = block_min_u64<VT_NW>(wave_min_u64_dpp(m), red + 2 * VT_NW, w);
+          const int64_t ms = (int64_t)(m ^ SIGN64);
+          const uint64_t b2 = (act && spc == ms) ? (uint64_t)lo : ~0ull;
+          g = block_min_u64<VT_NW>(wave_min_u64_dpp(b2), red + 3 * VT_NW, w);
+          g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+          minVal = ms;
+          ++fallbacks;
+        } else {
+          minVal = minVal + ((int64_t)hi - KEY_BIAS);
+        }
+        const bool assigned = (g >> 20) & 1u;
+        const int pk = (int)((g >> 10) & 1023u);
+        const int aux = (int)(g & 1023u);
+        const int pstar = assigned ? pk : 1023 - pk;
+        const int last = nrem - 1;
+        pos = (pos == pstar) ? -1 : ((pos == last) ? pstar : pos);
+        --nrem;
+        if (!assigned) {
+          sink = aux;
+          break;
+        }
+        i = aux;
+        // row i is reached with minimum minVal: u~[i] -= minVal now, += the
+        // final minimum at the end (scipy: u[i] += minVal - spc[col4row[i]]).
+        U.add_owner(i, -minVal);
+        vis |= ((i & 63) == lane) ? (1u << (i >> 6)) : 0u;
+      }
+      // dual updates: visited rows (this wave's copy), visited columns (owner)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if ((vis >> k) & 1u) {
+          const uint64_t v = (((uint64_t)U.hi[k] << 32) | U.lo[k]) + (uint64_t)minVal;
+          U.lo[k] = (uint32_t)v;
+          U.hi[k] = (uint32_t)(v >> 32);
+        }
+      }
+      if (live && pos < 0) {
+        nv = nv + (minVal - spc);
+        path_l[j] = (int16_t)path;
+      }
+      __syncthreads();
+      if (tid == 0) {  // augment along the path from the sink back to cur
+        int jj = sink;
+        for (;;) {
+          const int pi = path_l[jj];
+          r4c_l[jj] = (int16_t)pi;
+          const int t = c4r_l[pi];
+          c4r_l[pi] = (int16_t)jj;
+          jj = t;
+          if (pi == cur) break;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // -- outputs (column-owner view): thread j knows row r4c[j] took column j ----------
+  int64_t cost = 0, dch = 0, dgh = 0;
+  if (live) {
+    // code(row, j) for a per-lane row: scan the column once (static indices)
+    const int rn = r4c_l[j];
+    uint32_t vn = 0, vo = 0;
+#pragma unroll
+    for (int q = 0; q < RegTile<MODE>::DW; ++q) {
+      uint32_t dw;
+      if constexpr (MODE == 0) dw = (q < 32) ? T.a[q] : T.b[q - 32];
+      else dw = (q < 32) ? T.a[q] : (q < 64) ? T.b[q - 32] : (q < 96) ? T.c[q - 64] : T.d[q - 96];
+      const int rpd = RegTile<MODE>::ROWS_PER_DW;
+      const int bits = 32 / rpd;
+      if (rn / rpd == q) vn = (dw >> (bits * (rn % rpd))) & ((1u << bits) - 1u);
+      if (j / rpd == q) vo = (dw >> (bits * (j % rpd))) & ((1u << bits) - 1u);
+    }
+    const int tn = ctype[j];
+    if (MODE == 0) {
+      cost += single_cost(vn, nw1, a.E);
+      dch += child_happy(vn, nw1) - child_happy(vo, nw1);
+      dgh += gift_happy(a, rows_l[rn], tn) - gift_happy(a, rows_l[j], tn);
+    } else {
+      cost += twin_cost(vn, nw1, a.E);
+      dch += child_happy(vn & 0xFF, nw1) + child_happy(vn >> 8, nw1) -
+             child_happy(vo & 0xFF, nw1) - child_happy(vo >> 8, nw1);
+      dgh += gift_happy(a, rows_l[rn], tn) + gift_happy(a, rows_l[rn] + 1, tn) -
+             gift_happy(a, rows_l[j], tn) - gift_happy(a, rows_l[j] + 1, tn);
+    }
+  }
+  cost = wave_sum_i64(cost);
+  dch = wave_sum_i64(dch);
+  dgh = wave_sum_i64(dgh);
+  if (lane == 0) {
+    part[3 * w + 0] = cost;
+    part[3 * w + 1] = dch;
+    part[3 * w + 2] = dgh;
+  }
+  // apply: row i's child receives the type of column col[i] (all read from
+  // LDS copies taken before any store, so the in-place update is race-free)
+  if (live) {
+    const int col = c4r_l[j];  // here j plays the row
+    if (a.col) a.col[(size_t)b * n + j] = col;
+    const int16_t tnew = ctype[col];
+    a.types[rows_l[j]] = tnew;
+    if (MODE) a.types[rows_l[j] + 1] = tnew;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int64_t tc = 0, td0 = 0, td1 = 0;
+    for (int q = 0; q < VT_NW; ++q) {
+      tc += part[3 * q];
+      td0 += part[3 * q + 1];
+      td1 += part[3 * q + 2];
+    }
+    if (a.cost) a.cost[b] = tc;
+    if (a.steps) a.steps[b] = steps;
+    if (a.delta) {
+      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)td0);
+      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)td1);
+    }
+    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generic batched LSAP.  int64 paths use the multi-wave solver (rows streamed
 // from global memory, or generated by hash); float64 uses the single-wave
 // scipy-replay solver sap_solve<K, double>.
@@ -1208,6 +1619,14 @@ int launch_santa(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
+template <int MODE>
+int launch_santa_vt(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
+  const VtLds L = vt_lds_layout(ctx->ng);
+  if (L.total > 64 * 1024) return fail(SH_ERR_ARGS, "too many gift types for the LDS chain heads");
+  hipLaunchKernelGGL((santa_vt_kernel<MODE>), dim3(B), dim3(VT_WG), L.total, s, a);
+  HIP_TRY(hipGetLastError());
+  return SH_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -1226,7 +1645,11 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   a.err = ctx->d_err; a.E = ctx->E; a.n = n; a.nc = ctx->nc; a.ng = ctx->ng;
   a.n_wish = ctx->n_wish; a.n_good = ctx->n_good; a.flags = flags;
   hipStream_t s = (hipStream_t)stream;
-  return mode == SH_MODE_SINGLE ? launch_santa<1, 0>(ctx, a, B, s) : launch_santa<1, 1>(ctx, a, B, s);
+  if (flags & SH_FLAG_LDS_TILE)
+    return mode == SH_MODE_SINGLE ? launch_santa<1, 0>(ctx, a, B, s) : launch_santa<1, 1>(ctx, a, B, s);
+  // twins keep the LDS tile: their 128-dword register column does not stay
+  // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
+  return mode == SH_MODE_SINGLE ? launch_santa_vt<0>(ctx, a, B, s) : launch_santa<1, 1>(ctx, a, B, s);
 }
 
 int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream) {

@@ -304,3 +304,24 @@ def test_no_fallback_on_santa_rounds(sh, ctx, full_data):
         rows = ctx.sample_blocks(mode, n, min(nb, 512), 5, 0)
         ctx.solve_blocks(mode, rows, n, types)
     assert ctx.fallback_steps() == 0
+
+
+def test_register_and_lds_tile_kernels_agree(sh, ctx, full_data):
+    """The register-tile kernel (default for singles) and the LDS-tile kernel
+    (SH_FLAG_LDS_TILE) produce identical rounds."""
+    from santa_hip import _lib
+    mode, n = 0, 256
+    for B, nn in ((64, 256), (16, 100), (8, 37)):
+        rows = ctx.sample_blocks(mode, nn, B, 77, 9)
+        outs = []
+        for fl in (0, _lib.SH_FLAG_LDS_TILE):
+            types = ctx.upload_types(full_data.types)
+            col = torch.empty(B * nn, dtype=torch.int32, device="cuda")
+            cost = torch.empty(B, dtype=torch.int64, device="cuda")
+            delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+            steps = torch.empty(B, dtype=torch.int64, device="cuda")
+            ctx.solve_blocks(mode, rows, nn, types, col=col, cost=cost, delta=delta, steps=steps,
+                             flags=fl)
+            outs.append([x.cpu().numpy() for x in (col, cost, delta, steps, types)])
+        for x, y in zip(*outs):
+            assert np.array_equal(x, y)

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=0, help="0 = full round")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--phase", choices=["all", "build", "solve"], default="all")
+    ap.add_argument("--flags", type=int, default=0, help="extra SH_FLAG_* bits (8 = LDS tile)")
     a = ap.parse_args()
     sd = D.synthetic(2017)
     ctx = SantaGPU.from_data(sd, 0)
@@ -39,7 +40,7 @@ def main():
             t = base.clone()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            ctx.solve_blocks(a.mode, rows, a.n, t, steps=steps, flags=fl)
+            ctx.solve_blocks(a.mode, rows, a.n, t, steps=steps, flags=fl | a.flags)
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
