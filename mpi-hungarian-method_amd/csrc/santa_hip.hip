@@ -1216,6 +1216,343 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
 }
 
 // ---------------------------------------------------------------------------
+// Single-wave register kernel (singles, n <= 256): the production path.
+//
+// One wave64 per block, lane l owns columns l + 64k (k < 4).  Everything the
+// Dijkstra loop touches is in registers:
+//   tile  256 dwords per lane: dword r = the uint8 codes of the lane's four
+//         columns at row r, read with a wave-uniform r (s_set_gpr_idx);
+//   duals u (row r in lane r&63, slot r>>6), -v and spc/pos/path/row4col per
+//         owned column, col4row per owned row;
+// cross-lane values move with readlane, so a step has no LDS access and no
+// barrier.  The row-dual bookkeeping is the per-wave scheme of the
+// register-tile kernel above (u~[i] -= m when row i is reached, += final
+// minimum at the end), and the argmin is the same packed key, one 64-bit
+// wave-min per step.  The block cost is sum(u) + sum(v) (complementary
+// slackness holds exactly in integer arithmetic for the matched pairs), and a
+// matched entry's code is recovered from its reduced-cost identity
+// C[i][col] = u[i] + v[col].  1 wave per SIMD (~310 VGPRs), 4 blocks per CU.
+// ---------------------------------------------------------------------------
+constexpr int SW_REG_ROWS = 128;  // tile rows held in VGPRs; the rest in LDS
+
+struct SwLds {
+  size_t tile, rows, ctype, head, nxt, total;
+};
+
+__host__ __device__ __forceinline__ SwLds sw_lds_layout(int ng) {
+  SwLds L;
+  size_t off = 0;
+  L.tile = off;  off += (size_t)128 * 256;  // rows 128..255 [row][lane*4 + k]; stage for 0..127
+  L.rows = off;  off += 256 * 4;
+  L.ctype = off; off += 256 * 2;
+  L.head = off;  off += r16((size_t)ng * 4);
+  L.nxt = off;   off += 256 * 2;
+  L.total = off;
+  return L;
+}
+
+// dword r (< 128) of the register tile = codes of columns (l, l+64, l+128,
+// l+192) at row r; r wave-uniform.  By-value vectors (not a struct member
+// access through `this`) so that SROA keeps them in VGPRs.
+__device__ __forceinline__ uint32_t tile128_get(u32x32 v0, u32x32 v1, u32x32 v2, u32x32 v3, int r) {
+  const int x = r & 31, q = r >> 5;
+  uint32_t w0 = v0[x], w1 = v1[x], w2 = v2[x], w3 = v3[x];
+  asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
+  const uint32_t a = (q & 1) ? w1 : w0, b = (q & 1) ? w3 : w2;
+  return (q & 2) ? b : a;
+}
+
+template <typename A>
+__device__ __forceinline__ A pick4(const A (&arr)[4], int k) {  // k wave-uniform
+  A x0 = arr[0], x1 = arr[1], x2 = arr[2], x3 = arr[3];
+  asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+  const A a = (k & 1) ? x1 : x0, b = (k & 1) ? x3 : x2;
+  return (k & 2) ? b : a;
+}
+
+__device__ __forceinline__ int64_t readlane_i64(int64_t x, int l) {
+  return (int64_t)readlane_u64((uint64_t)x, l);
+}
+
+__global__ __launch_bounds__(WAVE, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void santa_sw_kernel(SantaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int n = a.n;
+  const SwLds L = sw_lds_layout(a.ng);
+  uint8_t *ltile = smem + L.tile;
+  const uint32_t *ltile32 = (const uint32_t *)ltile;
+  int32_t *rows_l = (int32_t *)(smem + L.rows);
+  int16_t *ctype = (int16_t *)(smem + L.ctype);
+  int32_t *head = (int32_t *)(smem + L.head);
+  int16_t *nxt = (int16_t *)(smem + L.nxt);
+
+  // -- rows, range check, chains ------------------------------------------------
+  int bad = 0;
+  for (int j = lane; j < n; j += WAVE) {
+    const int r = a.rows[(size_t)b * n + j];
+    bad |= (r < 0) || (r >= a.nc);
+    rows_l[j] = r;
+  }
+  if (__any(bad)) {
+    if (lane == 0) atomicOr(a.err, 1);
+    return;
+  }
+  for (int t = lane; t < a.ng; t += WAVE) head[t] = -1;
+  __syncthreads();
+  for (int j = lane; j < n; j += WAVE) {
+    const int16_t ty = a.types[rows_l[j]];
+    ctype[j] = ty;
+    nxt[j] = (int16_t)atomicExch(&head[ty], j);
+  }
+  __syncthreads();
+
+  // -- build: rows 0..127 staged in the LDS tile area and moved to VGPRs, then
+  //    rows 128..255 built in place (they stay in LDS) -------------------------
+  const int nw = a.n_wish;
+  const int nw1 = nw + 1;
+  u32x32 v0, v1, v2, v3;
+  uint32_t oldcode[4];  // code(row l+64k, column l+64k): the row's own gift
+  {
+    const bool vec = (nw & 3) == 0;
+    const int cpr = vec ? (nw >> 2) : nw;
+    auto put = [&](int lr, int r, int gift) {
+      for (int jj = head[gift]; jj >= 0; jj = nxt[jj])
+        ltile[lr * 256 + (jj & 63) * 4 + (jj >> 6)] = (uint8_t)(r + 1);
+    };
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int r0 = g * 128;
+      if (r0 < n) {
+#pragma unroll
+        for (int q = 0; q < 32; ++q) ((uint4 *)ltile)[q * WAVE + lane] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        const int rows_here = min(128, n - r0);
+        const int units = rows_here * cpr;
+        if (vec) {
+          constexpr int U = 8;
+          for (int base = 0; base < units; base += WAVE * U) {
+            uint2 q[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const int c = base + u * WAVE + lane;
+              if (c < units) {
+                const int lr = c / cpr, cc = c - lr * cpr;
+                q[u] = *(const uint2 *)(a.wish + (size_t)rows_l[r0 + lr] * nw + 4 * cc);
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const int c = base + u * WAVE + lane;
+              if (c < units) {
+                const int lr = c / cpr, cc = c - lr * cpr;
+                put(lr, 4 * cc + 0, (int16_t)(q[u].x & 0xFFFFu));
+                put(lr, 4 * cc + 1, (int16_t)(q[u].x >> 16));
+                put(lr, 4 * cc + 2, (int16_t)(q[u].y & 0xFFFFu));
+                put(lr, 4 * cc + 3, (int16_t)(q[u].y >> 16));
+              }
+            }
+          }
+        } else {
+          for (int c = lane; c < units; c += WAVE) {
+            const int lr = c / nw, r = c - lr * nw;
+            put(lr, r, a.wish[(size_t)rows_l[r0 + lr] * nw + r]);
+          }
+        }
+        __syncthreads();
+        // own-gift codes of rows r0 + lane (+64): column lane + 64k, k = 2g, 2g+1
+        oldcode[2 * g] = (ltile32[lane * WAVE + lane] >> (16 * g)) & 0xFFu;
+        oldcode[2 * g + 1] = (ltile32[(lane + 64) * WAVE + lane] >> (16 * g + 8)) & 0xFFu;
+        if (g == 0) {
+#pragma unroll
+          for (int x = 0; x < 32; ++x) {
+            v0[x] = ltile32[x * WAVE + lane];
+            v1[x] = ltile32[(x + 32) * WAVE + lane];
+            v2[x] = ltile32[(x + 64) * WAVE + lane];
+            v3[x] = ltile32[(x + 96) * WAVE + lane];
+          }
+          __syncthreads();
+        }
+      } else {
+        oldcode[2 * g] = oldcode[2 * g + 1] = 0;
+      }
+    }
+  }
+
+// -- solve -----------------------------------------------------------------------
+  const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
+  const int64_t INF = INT64_MAX;
+  int64_t spc[4], nv[4], ur[4];  // ur: u~ of rows lane+64k
+  int path[4], pos[4], r4c[4], c4r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    nv[k] = 0;
+    ur[k] = 0;
+    path[k] = -1;
+    r4c[k] = -1;
+    c4r[k] = -1;
+  }
+  int64_t steps = 0;
+  int fallbacks = 0;
+  if (a.flags & SH_FLAG_BUILD_ONLY) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c4r[k] = r4c[k] = lane + WAVE * k;
+  } else {
+    for (int cur = 0; cur < n; ++cur) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int j = lane + WAVE * k;
+        spc[k] = INF;
+        pos[k] = (j < n) ? (n - 1 - j) : -1;
+      }
+      uint32_t vis = ((cur & 63) == lane) ? (1u << (cur >> 6)) : 0u;
+      int nrem = n;
+      int64_t minVal = 0;
+      int i = cur;
+      int sink;
+      for (;;) {
+        ++steps;
+        uint32_t w;
+        if (i < SW_REG_ROWS)
+          w = tile128_get(v0, v1, v2, v3, i);
+        else
+          w = ltile32[(i - SW_REG_ROWS) * WAVE + lane];
+        const int64_t ui = readlane_i64(pick4(ur, i >> 6), i & 63);
+        const uint64_t kb = (uint64_t)KEY_BIAS - (uint64_t)minVal;
+        uint64_t best = ~0ull;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int j = lane + WAVE * k;
+          const int64_t r = single_cost((w >> (8 * k)) & 0xFFu, nw1, a.E) + nv[k] - ui;
+          const bool act = pos[k] >= 0;
+          const bool upd = act && (r < spc[k]);
+          spc[k] = upd ? r : spc[k];
+          path[k] = upd ? i : path[k];
+          const uint32_t lo = (r4c[k] < 0) ? (((uint32_t)(1023 - pos[k]) << 10) | (uint32_t)j)
+                                           : ((1u << 20) | ((uint32_t)pos[k] << 10) | (uint32_t)r4c[k]);
+          const uint64_t key = (key_hi_of((uint64_t)spc[k] + kb) << KEY_LO_BITS) | lo;
+          best = umin64(best, act ? key : ~0ull);
+        }
+        uint64_t g = wave_min_u64_fast(best);
+        // asm results are treated as divergent: make the winner provably uniform
+        g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+        const uint64_t hi = g >> KEY_LO_BITS;
+        if (exact || hi == 0 || hi == KEY_HI_MAX) {
+          uint64_t m = ~0ull;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (pos[k] >= 0) m = umin64(m, (uint64_t)spc[k] ^ SIGN64);
+          m = wave_min_u64_dpp(m);
+          const int64_t ms = (int64_t)(m ^ SIGN64);
+          uint64_t b2 = ~0ull;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int j = lane + WAVE * k;
+            if (pos[k] >= 0 && spc[k] == ms) {
+              const uint32_t lo = (r4c[k] < 0)
+                                      ? (((uint32_t)(1023 - pos[k]) << 10) | (uint32_t)j)
+                                      : ((1u << 20) | ((uint32_t)pos[k] << 10) | (uint32_t)r4c[k]);
+              b2 = umin64(b2, lo);
+            }
+          }
+          g = wave_min_u64_dpp(b2);
+          g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+          minVal = ms;
+          ++fallbacks;
+        } else {
+          minVal = minVal + ((int64_t)hi - KEY_BIAS);
+        }
+        const bool assigned = (g >> 20) & 1u;
+        const int pk = (int)((g >> 10) & 1023u);
+        const int aux = (int)(g & 1023u);
+        const int pstar = assigned ? pk : 1023 - pk;
+        const int last = nrem - 1;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int p = pos[k];
+          pos[k] = (p == pstar) ? -1 : ((p == last) ? pstar : p);
+        }
+        --nrem;
+        if (!assigned) {
+          sink = aux;
+          break;
+        }
+        i = __builtin_amdgcn_readfirstlane(aux);
+        if ((i & 63) == lane) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if ((i >> 6) == k) ur[k] -= minVal;
+        }
+        vis |= ((i & 63) == lane) ? (1u << (i >> 6)) : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if ((vis >> k) & 1u) ur[k] += minVal;
+        const int j = lane + WAVE * k;
+        if (j < n && pos[k] < 0) nv[k] = nv[k] + (minVal - spc[k]);
+      }
+      // augment along path[] from the sink back to cur (registers only)
+      int j = sink;
+      for (;;) {
+        const int pi = __builtin_amdgcn_readlane(pick4(path, j >> 6), j & 63);
+        const int t = __builtin_amdgcn_readlane(pick4(c4r, pi >> 6), pi & 63);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (lane + WAVE * k == j) r4c[k] = pi;
+          if (lane + WAVE * k == pi) c4r[k] = j;
+        }
+        j = t;
+        if (pi == cur) break;
+      }
+    }
+  }
+
+  // -- outputs: lane handles rows i = lane + 64k --------------------------------------
+  int64_t cost = 0, dch = 0, dgh = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    // v of column c4r[k] from its owner lane (per-lane source: ds_bpermute)
+    const int col = c4r[k] < 0 ? 0 : c4r[k];
+    int64_t vq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vq[q] = __shfl(-nv[q], col & 63, WAVE);
+    const int cs = col >> 6;
+    const int64_t vcol = (cs == 0) ? vq[0] : (cs == 1) ? vq[1] : (cs == 2) ? vq[2] : vq[3];
+    const int i = lane + WAVE * k;
+    if (i < n) {
+      const int64_t cij = ur[k] + vcol;  // = C[i][col] (tight matched edge)
+      const uint32_t cn = (cij == a.E) ? 0u : (uint32_t)((cij >> 32) + nw1);
+      const uint32_t co = oldcode[k];
+      const int child = rows_l[i];
+      const int told = ctype[i], tnew = ctype[col];
+      if (a.flags & SH_FLAG_BUILD_ONLY) {
+        cost += single_cost(co, nw1, a.E);
+      } else {
+        cost += cij;
+        dch += child_happy(cn, nw1) - child_happy(co, nw1);
+        dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
+      }
+      if (a.col) a.col[(size_t)b * n + i] = col;
+      a.types[child] = (int16_t)tnew;  // this block owns child; ctype holds old types
+    }
+  }
+  cost = wave_sum_i64(cost);
+  dch = wave_sum_i64(dch);
+  dgh = wave_sum_i64(dgh);
+  if (lane == 0) {
+    if (a.cost) a.cost[b] = cost;
+    if (a.steps) a.steps[b] = steps;
+    if (a.delta) {
+      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
+      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
+    }
+    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generic batched LSAP.  int64 paths use the multi-wave solver (rows streamed
 // from global memory, or generated by hash); float64 uses the single-wave
 // scipy-replay solver sap_solve<K, double>.
@@ -1619,6 +1956,14 @@ int launch_santa(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
+int launch_santa_sw(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
+  const SwLds L = sw_lds_layout(ctx->ng);
+  if (L.total > 64 * 1024) return fail(SH_ERR_ARGS, "too many gift types for the LDS chain heads");
+  hipLaunchKernelGGL(santa_sw_kernel, dim3(B), dim3(WAVE), L.total, s, a);
+  HIP_TRY(hipGetLastError());
+  return SH_OK;
+}
+
 template <int MODE>
 int launch_santa_vt(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   const VtLds L = vt_lds_layout(ctx->ng);
@@ -1649,7 +1994,9 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
     return mode == SH_MODE_SINGLE ? launch_santa<1, 0>(ctx, a, B, s) : launch_santa<1, 1>(ctx, a, B, s);
   // twins keep the LDS tile: their 128-dword register column does not stay
   // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
-  return mode == SH_MODE_SINGLE ? launch_santa_vt<0>(ctx, a, B, s) : launch_santa<1, 1>(ctx, a, B, s);
+  if (mode == SH_MODE_TWINS) return launch_santa<1, 1>(ctx, a, B, s);
+  if (flags & SH_FLAG_VT_TILE) return launch_santa_vt<0>(ctx, a, B, s);
+  return launch_santa_sw(ctx, a, B, s);
 }
 
 int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream) {

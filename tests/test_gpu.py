@@ -306,15 +306,16 @@ def test_no_fallback_on_santa_rounds(sh, ctx, full_data):
     assert ctx.fallback_steps() == 0
 
 
-def test_register_and_lds_tile_kernels_agree(sh, ctx, full_data):
-    """The register-tile kernel (default for singles) and the LDS-tile kernel
-    (SH_FLAG_LDS_TILE) produce identical rounds."""
+def test_kernel_designs_agree(sh, ctx, full_data):
+    """The single-wave register kernel (default for singles), the 4-wave
+    register-tile kernel (SH_FLAG_VT_TILE) and the LDS-tile kernel
+    (SH_FLAG_LDS_TILE) produce identical rounds: col, cost, deltas, steps, state."""
     from santa_hip import _lib
-    mode, n = 0, 256
-    for B, nn in ((64, 256), (16, 100), (8, 37)):
+    mode = 0
+    for B, nn in ((64, 256), (16, 100), (8, 37), (8, 130), (4, 1)):
         rows = ctx.sample_blocks(mode, nn, B, 77, 9)
         outs = []
-        for fl in (0, _lib.SH_FLAG_LDS_TILE):
+        for fl in (0, _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_LDS_TILE):
             types = ctx.upload_types(full_data.types)
             col = torch.empty(B * nn, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -323,5 +324,6 @@ def test_register_and_lds_tile_kernels_agree(sh, ctx, full_data):
             ctx.solve_blocks(mode, rows, nn, types, col=col, cost=cost, delta=delta, steps=steps,
                              flags=fl)
             outs.append([x.cpu().numpy() for x in (col, cost, delta, steps, types)])
-        for x, y in zip(*outs):
-            assert np.array_equal(x, y)
+        for other in outs[1:]:
+            for x, y in zip(outs[0], other):
+                assert np.array_equal(x, y), (B, nn)
