@@ -14,6 +14,7 @@ whole job; score gain per second is reported beside it.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -192,7 +193,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (seeded Kaggle-shaped: 1M children x 100 wishes, 1000 gifts x 1000 good kids)",
@@ -205,7 +206,8 @@ def main():
         "score_end": state["best"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": f"santa_block_kernel<K=4,MODE={mode}>",
+                     "kernel": ("santa_vt_kernel<0> (4-wave register tile)" if mode == 0
+                                else "santa_block_kernel<1,1> (4-wave LDS tile)"),
                      "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                      "algorithmic_bytes_per_block": per_block,
                      "lds": {"bytes_per_launch": lds_bytes,
@@ -213,6 +215,20 @@ def main():
                              "peak_GBs": LDS_PEAK_GBS},
                      "dijkstra_steps_per_launch": dsteps},
     }
+    # HBM traffic of the same kernel from the committed rocprofv3 PMC passes
+    # (tools/profile_round.sh -> profiles/<tag>_summary.json; FETCH_SIZE and
+    # WRITE_SIZE in separate passes, KB x 1024, on a full 3730-block round)
+    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))
+    if prof and mode == 0:
+        try:
+            hb = json.load(open(prof[-1]))["hbm_bytes_per_launch"]
+            kname = out["roofline"]["kernel"].split(" ")[0].split("<")[0]
+            e = hb.get(kname, {})
+            if "FETCH_SIZE_bytes" in e and "WRITE_SIZE_bytes" in e:
+                out["roofline"]["traffic"] = e["FETCH_SIZE_bytes"] + e["WRITE_SIZE_bytes"]
+                out["roofline"]["traffic_source"] = os.path.basename(prof[-1])
+        except (OSError, KeyError, ValueError):
+            pass
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sd, mode, n, args.cpu_seconds)
     if rank == 0:

@@ -45,9 +45,10 @@ extern "C" {
 #define SH_FLAG_EXACT_ARGMIN 2u /* always use the two-pass exact argmin    */
 #define SH_FLAG_BUILD_ONLY 4u   /* sh_solve_blocks: build the cost tiles and
                                    apply the identity (phase timing only)  */
-#define SH_FLAG_LDS_TILE 8u     /* sh_solve_blocks: earlier kernel designs  */
-#define SH_FLAG_VT_TILE 16u     /* (LDS tile / 4-wave register tile), kept
-                                   for A/B profiling; same results         */
+#define SH_FLAG_LDS_TILE 8u     /* sh_solve_blocks, singles: alternative    */
+#define SH_FLAG_SW_TILE 16u     /* kernel designs (4-wave LDS tile / one-
+                                   wave register tile) kept for A/B
+                                   profiling; identical results            */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024

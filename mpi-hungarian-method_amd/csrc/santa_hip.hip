@@ -1995,8 +1995,8 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   // twins keep the LDS tile: their 128-dword register column does not stay
   // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
   if (mode == SH_MODE_TWINS) return launch_santa<1, 1>(ctx, a, B, s);
-  if (flags & SH_FLAG_VT_TILE) return launch_santa_vt<0>(ctx, a, B, s);
-  return launch_santa_sw(ctx, a, B, s);
+  if (flags & SH_FLAG_SW_TILE) return launch_santa_sw(ctx, a, B, s);
+  return launch_santa_vt<0>(ctx, a, B, s);
 }
 
 int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream) {

@@ -22,7 +22,7 @@ SH_COMPAT_TIEBREAK = 1
 SH_FLAG_EXACT_ARGMIN = 2
 SH_FLAG_BUILD_ONLY = 4
 SH_FLAG_LDS_TILE = 8
-SH_FLAG_VT_TILE = 16
+SH_FLAG_SW_TILE = 16
 SH_MAX_N = 1024
 SH_MAX_N_SANTA = 256
 

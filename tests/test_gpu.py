@@ -307,15 +307,15 @@ def test_no_fallback_on_santa_rounds(sh, ctx, full_data):
 
 
 def test_kernel_designs_agree(sh, ctx, full_data):
-    """The single-wave register kernel (default for singles), the 4-wave
-    register-tile kernel (SH_FLAG_VT_TILE) and the LDS-tile kernel
+    """The 4-wave register-tile kernel (default for singles), the one-wave
+    register kernel (SH_FLAG_SW_TILE) and the 4-wave LDS-tile kernel
     (SH_FLAG_LDS_TILE) produce identical rounds: col, cost, deltas, steps, state."""
     from santa_hip import _lib
     mode = 0
     for B, nn in ((64, 256), (16, 100), (8, 37), (8, 130), (4, 1)):
         rows = ctx.sample_blocks(mode, nn, B, 77, 9)
         outs = []
-        for fl in (0, _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_LDS_TILE):
+        for fl in (0, _lib.SH_FLAG_SW_TILE, _lib.SH_FLAG_LDS_TILE):
             types = ctx.upload_types(full_data.types)
             col = torch.empty(B * nn, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")

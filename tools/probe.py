@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--blocks", type=int, default=0, help="0 = full round")
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--phase", choices=["all", "build", "solve"], default="all")
+    ap.add_argument("--phase", choices=["all", "build", "solve", "score"], default="all")
     ap.add_argument("--flags", type=int, default=0, help="extra SH_FLAG_* bits (8 = LDS tile)")
     a = ap.parse_args()
     sd = D.synthetic(2017)
@@ -45,6 +45,16 @@ def main():
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
         out[name] = {"ms": min(ts), "all_ms": ts}
+    if a.phase in ("all", "score"):
+        ts = []
+        for _ in range(a.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ctx.score_sums_async(base)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        out["score"] = {"ms": min(ts), "all_ms": ts}
     out["blocks"] = B
     out["steps_total"] = int(steps.sum())
     out["steps_per_block"] = int(steps.sum()) / B

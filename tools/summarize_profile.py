@@ -1,0 +1,79 @@
+"""Turn a tools/profile_round.sh output directory into profiles/<tag>_*.
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim) and
+profiles/<tag>_summary.json: per-kernel average duration from the trace,
+HBM bytes per launch from FETCH_SIZE / WRITE_SIZE (KB, x1024), and the SQ
+counters per wave and per Dijkstra step of the block kernel."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def pmc(path):
+    agg = defaultdict(lambda: defaultdict(float))
+    for f in glob.glob(path):
+        for r in csv.DictReader(open(f)):
+            agg[r["Kernel_Name"]][r["Counter_Name"]] += float(r["Counter_Value"])
+    return agg
+
+
+def short(name):
+    for key in ("santa_vt_kernel", "santa_sw_kernel", "santa_block_kernel", "score_kernel",
+                "sample_kernel", "lsap_i64_kernel", "lsap_f64_kernel"):
+        if key in name:
+            return key
+    return name[:60]
+
+
+def main(src, tag, root):
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace_kernel_stats.csv"))
+    if stats:
+        shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    trace = defaultdict(list)
+    for f in glob.glob(os.path.join(src, "trace_kernel_trace.csv")):
+        for r in csv.DictReader(open(f)):
+            trace[short(r["Kernel_Name"])].append(
+                (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    out = {"tag": tag, "trace_ms": {k: {"calls": len(v), "avg_ms": sum(v) / len(v),
+                                         "min_ms": min(v), "max_ms": max(v)}
+                                     for k, v in trace.items()}}
+    fetch = pmc(os.path.join(src, "fetch_counter_collection.csv"))
+    write = pmc(os.path.join(src, "write_counter_collection.csv"))
+    fscore = pmc(os.path.join(src, "fetch_score_counter_collection.csv"))
+    hbm = {}
+    for d, key in ((fetch, "FETCH_SIZE"), (write, "WRITE_SIZE"), (fscore, "FETCH_SIZE")):
+        for k, v in d.items():
+            hbm.setdefault(short(k), {})[key + "_bytes"] = v.get(key, 0.0) * 1024
+    out["hbm_bytes_per_launch"] = hbm
+    probe = {}
+    pj = os.path.join(src, "probe_sq1.json")
+    if os.path.exists(pj):
+        probe = json.loads(open(pj).read().strip().splitlines()[-1])
+    sq = pmc(os.path.join(src, "sq1_counter_collection.csv"))
+    for k, v in pmc(os.path.join(src, "sq2_counter_collection.csv")).items():
+        sq[k].update(v)
+    steps = probe.get("steps_total")
+    sqs = {}
+    for k, v in sq.items():
+        waves = v.get("SQ_WAVES", 0) or 1
+        e = {c: x for c, x in v.items()}
+        if steps:
+            wps = steps * waves / probe["blocks"]
+            e["per_wave_step_quadcycles"] = {c: x / wps for c, x in v.items() if c.startswith("SQ_")
+                                             and c != "SQ_WAVES"}
+        sqs[short(k)] = e
+    out["sq"] = sqs
+    out["probe"] = probe
+    json.dump(out, open(os.path.join(prof, f"{tag}_summary.json"), "w"), indent=1)
+    print(json.dumps(out["trace_ms"], indent=1))
+    print(json.dumps(hbm, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
