@@ -45,10 +45,13 @@ extern "C" {
 #define SH_FLAG_EXACT_ARGMIN 2u /* always use the two-pass exact argmin    */
 #define SH_FLAG_BUILD_ONLY 4u   /* sh_solve_blocks: build the cost tiles and
                                    apply the identity (phase timing only)  */
-#define SH_FLAG_LDS_TILE 8u     /* sh_solve_blocks, singles: alternative    */
-#define SH_FLAG_SW_TILE 16u     /* kernel designs (4-wave LDS tile / one-
-                                   wave register tile) kept for A/B
-                                   profiling; identical results            */
+#define SH_FLAG_LDS_TILE 8u     /* sh_solve_blocks, singles n <= 256:       */
+#define SH_FLAG_SW_TILE 16u     /* alternative kernel designs (4-wave LDS   */
+#define SH_FLAG_VT_TILE 32u     /* tile / one-wave register tile / 4-wave
+                                   register tile) kept for A/B profiling;
+                                   identical results.  Default: one-wave
+                                   sparse LDS tile (+ register-tile fallback
+                                   for blocks whose hit lists overflow)    */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024
@@ -125,6 +128,13 @@ int sh_score(sh_ctx *ctx, const int16_t *d_types, int64_t *d_sums, void *stream)
 /* Device-side error flags of the context (bit 0: a block had rows out of
  * range; bit 1: infeasible solve).  Synchronises `stream`; clears the flags. */
 int sh_ctx_error_flags(sh_ctx *ctx, void *stream);
+
+/* Tuning / test hook of the default singles kernel: LDS bytes per block
+ * (0 = default 20 KiB, i.e. 8 blocks per CU).  The per-row hit lists must fit
+ * in what is left after the fixed per-block state; blocks that do not fit
+ * are solved by the register-tile fallback launch (same results).  Returns
+ * the resulting hit-list capacity (entries, >= 0) or SH_ERR_ARGS.         */
+int sh_ctx_set_sparse_budget(sh_ctx *ctx, int bytes);
 
 /* Profiling counter: Dijkstra steps of sh_solve_blocks that took the exact
  * two-pass argmin (cost spreads beyond the packed key's 2^42-unit window, or

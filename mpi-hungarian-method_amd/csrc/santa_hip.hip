@@ -581,6 +581,15 @@ struct SantaArgs {
   int64_t E;              // miss value in units
   int n, nc, ng, n_wish, n_good;
   unsigned flags;
+  // sparse-tile kernel: hit-list capacity and the overflow list it appends to
+  int cap;
+  int32_t *ovf_cnt;       // [1]
+  int32_t *ovf_list;      // [B]
+  // fallback launch (santa_vt_kernel): block ids to solve, and the other
+  // parity's overflow counter, reset for the next round
+  const int32_t *blist;   // [*bcount] or null = every block
+  const int32_t *bcount;
+  int32_t *ovf_reset;
 };
 
 __device__ __forceinline__ int64_t gift_happy(const SantaArgs &a, int child, int t) {
@@ -919,8 +928,13 @@ __host__ __device__ __forceinline__ VtLds vt_lds_layout(int ng) {
 template <int MODE>
 __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(SantaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int b = blockIdx.x;
+  int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (a.blist) {  // fallback launch: solve only the listed blocks
+    if (b == 0 && tid == 0) *a.ovf_reset = 0;
+    if (b >= *a.bcount) return;
+    b = a.blist[b];
+  }
   const int n = a.n;
   const VtLds L = vt_lds_layout(a.ng);
   uint8_t *stage = smem + L.stage;
@@ -1553,6 +1567,387 @@ __global__ __launch_bounds__(WAVE, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 }
 
 // ---------------------------------------------------------------------------
+// Sparse-tile single-wave kernel (singles, n <= 256): the production path.
+//
+// One wave64 per block and no barrier inside the Dijkstra loop.  Lane l owns
+// columns 4l..4l+3 and rows 4l..4l+3.  About 90 % of a Santa tile is misses
+// (a child wishes 100 of 1000 types), so the rank-code tile lives in LDS as
+// per-row hit lists of (column, code) uint16 entries, ~26 per row on
+// Kaggle-shaped data (~13 KB per block).  A Dijkstra step expands row i into
+// a 256-byte LDS row buffer (one ds_write_b8 per hit); each lane reads the
+// dword holding its four codes and clears it.  Everything else a step
+// touches is in registers: spc / -v / path / position / key bits per owned
+// column, the row duals u~ and the rows' hit ranges per owned row (the u~
+// bookkeeping of santa_vt_kernel: u~[i] -= m when row i is reached, += the
+// final minimum for visited rows).  ~20 KB LDS per block -> 8 blocks per CU,
+// i.e. two waves per SIMD hiding each other's LDS and DPP latencies, with
+// about a third of the register-tile kernel's VALU work per Dijkstra step.
+// A block whose hit lists overflow the LDS capacity is left untouched and
+// appended to an overflow list; santa_vt_kernel (register tile, any hit
+// count) solves those in a second launch.  Decisions are scipy's, as in
+// every other kernel here.
+// ---------------------------------------------------------------------------
+constexpr int SP_UMAX = 4;  // wishlist chunks per lane per build group
+
+struct SpLds {
+  size_t rowbuf, rows, ctype, nxt, own, gcnt, off, head, hits, total;
+};
+
+__host__ __device__ __forceinline__ SpLds sp_lds_layout(int ng, int cap) {
+  SpLds L;
+  size_t o = 0;
+  L.rowbuf = o; o += 256;                // row buffer: code of column j at byte j
+  L.rows = o;   o += 256 * 4;            // child ids
+  L.ctype = o;  o += 256 * 2;            // column gift types (old)
+  L.nxt = o;    o += 256 * 2;            // type -> column chains
+  L.own = o;    o += 256;                // code(i, i): row i's own (old) gift
+  L.gcnt = o;   o += 64 * 4;             // per-row hit counters of a build group
+  L.off = o;    o += r16(257 * 2);       // hit-list offsets per row
+  L.head = o;   o += r16((size_t)((ng + 1) / 2) * 4);  // int16 chain heads
+  L.hits = o;   o += r16((size_t)cap * 2);
+  L.total = o;
+  return L;
+}
+
+// head[t] <- j, returns the previous head (int16 heads, two per dword).
+__device__ __forceinline__ int head_push(uint32_t *head32, int t, int j) {
+  uint32_t *w = head32 + (t >> 1);
+  const int sh = (t & 1) * 16;
+  uint32_t old = *w, assumed;
+  do {
+    assumed = old;
+    const uint32_t nw = (assumed & ~(0xFFFFu << sh)) | ((uint32_t)(uint16_t)j << sh);
+    old = atomicCAS(w, assumed, nw);
+  } while (old != assumed);
+  return (int)(int16_t)((assumed >> sh) & 0xFFFFu);
+}
+
+__device__ __forceinline__ int head_get(const uint32_t *head32, int t) {
+  return (int)(int16_t)((head32[t >> 1] >> ((t & 1) * 16)) & 0xFFFFu);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, WAVE);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int n = a.n;
+  const int cap = a.cap;
+  const SpLds L = sp_lds_layout(a.ng, cap);
+  uint8_t *rowbuf = smem + L.rowbuf;
+  uint32_t *rowbuf32 = (uint32_t *)(smem + L.rowbuf);
+  int32_t *rows_l = (int32_t *)(smem + L.rows);
+  int16_t *ctype = (int16_t *)(smem + L.ctype);
+  int16_t *nxt = (int16_t *)(smem + L.nxt);
+  uint8_t *own = smem + L.own;
+  uint32_t *gcnt = (uint32_t *)(smem + L.gcnt);
+  uint16_t *off = (uint16_t *)(smem + L.off);
+  uint32_t *head32 = (uint32_t *)(smem + L.head);
+  uint16_t *hits = (uint16_t *)(smem + L.hits);
+
+  // -- rows, range check, chains ------------------------------------------------
+  int bad = 0;
+  for (int j = lane; j < n; j += WAVE) {
+    const int r = a.rows[(size_t)b * n + j];
+    bad |= (r < 0) || (r >= a.nc);
+    rows_l[j] = r;
+  }
+  if (__any(bad)) {
+    if (lane == 0) atomicOr(a.err, 1);
+    return;
+  }
+  for (int t = lane; t < (a.ng + 1) / 2; t += WAVE) head32[t] = 0xFFFFFFFFu;
+  rowbuf32[lane] = 0;
+  ((uint32_t *)own)[lane] = 0;
+  gcnt[lane] = 0;
+  __syncthreads();
+  for (int j = lane; j < n; j += WAVE) {
+    const int ty = a.types[rows_l[j]];
+    ctype[j] = (int16_t)ty;
+    nxt[j] = (int16_t)head_push(head32, ty, j);
+  }
+  __syncthreads();
+
+  // -- build the hit lists, G rows at a time ---------------------------------------
+  // chunk = 4 wishes (8-byte load) when n_wish % 4 == 0, else 1 wish.
+  const int nw = a.n_wish;
+  const int nw1 = nw + 1;
+  const bool vec = (nw & 3) == 0;
+  const int cpr = vec ? (nw >> 2) : nw;          // chunks per row
+  const int wpc = vec ? 4 : 1;                   // wishes per chunk
+  const int G = min(64, max(1, (WAVE * SP_UMAX) / cpr));
+  int base = 0;
+  for (int r0 = 0; r0 < n; r0 += G) {
+    const int grows = min(G, n - r0);
+    const int gch = grows * cpr;
+    uint2 q[SP_UMAX];
+    int slot[SP_UMAX];
+#pragma unroll
+    for (int u = 0; u < SP_UMAX; ++u) {
+      const int c = lane + WAVE * u;
+      if (c < gch) {
+        const int row = r0 + c / cpr, cc = c - (c / cpr) * cpr;
+        const int16_t *src = a.wish + (size_t)rows_l[row] * nw;
+        if (vec) {
+          q[u] = *(const uint2 *)(src + 4 * cc);
+        } else {
+          q[u].x = (uint32_t)(uint16_t)src[cc] | 0xFFFF0000u;
+          q[u].y = 0xFFFFFFFFu;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SP_UMAX; ++u) {
+      const int c = lane + WAVE * u;
+      slot[u] = 0;
+      if (c < gch) {
+        const int row = r0 + c / cpr, cc = c - (c / cpr) * cpr;
+        int cnt = 0;
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          if (z < wpc) {
+            const int g = (int)(int16_t)(((z < 2 ? q[u].x : q[u].y) >> (16 * (z & 1))) & 0xFFFFu);
+            for (int jj = head_get(head32, g); jj >= 0; jj = nxt[jj]) {
+              ++cnt;
+              if (jj == row) own[row] = (uint8_t)(cc * wpc + z + 1);
+            }
+          }
+        }
+        slot[u] = cnt ? (int)(atomicAdd(&gcnt[row - r0], (uint32_t)cnt) | ((uint32_t)cnt << 16)) : 0;
+      }
+    }
+    __syncthreads();
+    const uint32_t v = (lane < grows) ? gcnt[lane] : 0u;
+    const uint32_t incl = wave_incl_scan_u32(v);
+    const int total = __builtin_amdgcn_readlane((int)incl, 63);
+    if (base + total > cap) {  // does not fit: leave the block to the fallback kernel
+      if (lane == 0) {
+        const int p = atomicAdd(a.ovf_cnt, 1);
+        a.ovf_list[p] = b;
+      }
+      return;
+    }
+    if (lane < grows) off[r0 + lane] = (uint16_t)(base + (int)(incl - v));
+    gcnt[lane] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < SP_UMAX; ++u) {
+      const int c = lane + WAVE * u;
+      if (c < gch && slot[u]) {
+        const int row = r0 + c / cpr, cc = c - (c / cpr) * cpr;
+        int p = (int)off[row] + (slot[u] & 0xFFFF);
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          if (z < wpc) {
+            const int g = (int)(int16_t)(((z < 2 ? q[u].x : q[u].y) >> (16 * (z & 1))) & 0xFFFFu);
+            const uint32_t code = (uint32_t)(cc * wpc + z + 1) << 8;
+            for (int jj = head_get(head32, g); jj >= 0; jj = nxt[jj]) hits[p++] = (uint16_t)(code | (uint32_t)jj);
+          }
+        }
+      }
+    }
+    base += total;
+  }
+  if (lane == 0) off[n] = (uint16_t)base;
+  __syncthreads();
+  uint32_t offr[4];  // hit range of row 4*lane + k: start | end << 16
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = 4 * lane + k;
+    offr[k] = (r < n) ? ((uint32_t)off[r] | ((uint32_t)off[r + 1] << 16)) : 0u;
+  }
+
+  // -- solve ----------------------------------------------------------------------
+  const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
+  const int64_t INF = INT64_MAX;
+  const int64_t E = a.E;
+  int64_t spc[4], nv[4], ur[4];  // nv = -v of owned columns; ur = u~ of owned rows
+  int path[4], pos[4], r4c[4], c4r[4];
+  uint32_t lo[4];
+  bool live[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    nv[k] = 0;
+    ur[k] = 0;
+    path[k] = -1;
+    r4c[k] = -1;
+    c4r[k] = -1;
+  }
+  int64_t steps = 0;
+  int fallbacks = 0;
+  if (a.flags & SH_FLAG_BUILD_ONLY) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c4r[k] = r4c[k] = 4 * lane + k;
+  } else {
+    for (int cur = 0; cur < n; ++cur) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int j = 4 * lane + k;
+        spc[k] = INF;
+        live[k] = j < n;
+        pos[k] = n - 1 - j;
+        lo[k] = (r4c[k] < 0) ? (((uint32_t)(1023 - pos[k]) << 10) | (uint32_t)j)
+                             : ((1u << 20) | ((uint32_t)pos[k] << 10) | (uint32_t)r4c[k]);
+      }
+      uint32_t vis = ((cur >> 2) == lane) ? (1u << (cur & 3)) : 0u;
+      int nrem = n;
+      int64_t minVal = 0;
+      int i = cur;
+      int sink;
+      for (;;) {
+        ++steps;
+        const int64_t ui = readlane_i64(pick4(ur, i & 3), i >> 2);
+        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)pick4(offr, i & 3), i >> 2);
+        // expand row i into the row buffer, read this lane's four codes, clear
+        for (int s = (int)(o & 0xFFFFu) + lane; s < (int)(o >> 16); s += WAVE) {
+          const uint32_t e = hits[s];
+          rowbuf[e & 0xFFu] = (uint8_t)(e >> 8);
+        }
+        const uint32_t w = rowbuf32[lane];
+        rowbuf32[lane] = 0;
+        // r = C[i][j] - u~[i] - v[j]:  C = code ? (code - nw1) * 2^32 : E
+        const uint64_t a1 = (uint64_t)(-ui);      // hit:  -u~ + (code - nw1) << 32
+        const uint64_t a0 = (uint64_t)(E - ui);   // miss: E - u~
+        const uint64_t kb = (uint64_t)KEY_BIAS - (uint64_t)minVal;
+        uint64_t best = ~0ull;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t code = (w >> (8 * k)) & 0xFFu;
+          const uint32_t tl = code ? (uint32_t)a1 : (uint32_t)a0;
+          const uint32_t th = code ? (uint32_t)(a1 >> 32) + code - (uint32_t)nw1 : (uint32_t)(a0 >> 32);
+          const int64_t r = nv[k] + (int64_t)(((uint64_t)th << 32) | tl);
+          const bool upd = live[k] && (r < spc[k]);
+          spc[k] = upd ? r : spc[k];
+          path[k] = upd ? i : path[k];
+          const uint64_t sb = (uint64_t)spc[k] + kb;
+          const uint32_t sh = (uint32_t)(sb >> 32), sl = (uint32_t)sb;
+          uint32_t kh = __builtin_amdgcn_alignbit(sh, sl, 11);
+          kh = (sh < 2048u) ? kh : ((int32_t)sh < 0 ? 0u : 0xFFFFFFFFu);
+          const uint64_t key = ((uint64_t)kh << 32) | ((sl << 21) | lo[k]);
+          best = (live[k] && key < best) ? key : best;
+        }
+        uint64_t g = wave_min_u64_fast(best);
+        g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+        const uint32_t ghi = (uint32_t)(g >> 32);
+        if (exact || ghi == 0u || ghi == 0xFFFFFFFFu) {
+          uint64_t m = ~0ull;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (live[k]) m = umin64(m, (uint64_t)spc[k] ^ SIGN64);
+          m = wave_min_u64_dpp(m);
+          const int64_t ms = (int64_t)(m ^ SIGN64);
+          uint64_t b2 = ~0ull;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (live[k] && spc[k] == ms) b2 = umin64(b2, (uint64_t)lo[k]);
+          g = wave_min_u64_dpp(b2);
+          g = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+          minVal = ms;
+          ++fallbacks;
+        } else {
+          minVal = minVal + ((int64_t)(g >> KEY_LO_BITS) - KEY_BIAS);
+        }
+        const uint32_t glo = (uint32_t)g & 0x1FFFFFu;
+        const bool assigned = (glo >> 20) & 1u;
+        const int pk = (int)((glo >> 10) & 1023u);
+        const int aux = (int)(glo & 1023u);
+        const int pstar = assigned ? pk : 1023 - pk;
+        const int last = nrem - 1;
+        const uint32_t X = (uint32_t)(last ^ pstar) << 10;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          live[k] = live[k] && (lo[k] != glo);
+          const bool mv = pos[k] == last;
+          pos[k] = mv ? pstar : pos[k];
+          lo[k] = mv ? (lo[k] ^ X) : lo[k];
+        }
+        --nrem;
+        if (!assigned) {
+          sink = aux;
+          break;
+        }
+        i = __builtin_amdgcn_readfirstlane(aux);
+        if ((i >> 2) == lane) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if ((i & 3) == k) ur[k] -= minVal;
+        }
+        vis |= ((i >> 2) == lane) ? (1u << (i & 3)) : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if ((vis >> k) & 1u) ur[k] += minVal;
+        if (4 * lane + k < n && !live[k]) nv[k] = nv[k] + (minVal - spc[k]);
+      }
+      // augment along path[] from the sink back to cur (registers only)
+      int j = sink;
+      for (;;) {
+        const int pi = __builtin_amdgcn_readlane(pick4(path, j & 3), j >> 2);
+        const int t = __builtin_amdgcn_readlane(pick4(c4r, pi & 3), pi >> 2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (4 * lane + k == j) r4c[k] = pi;
+          if (4 * lane + k == pi) c4r[k] = j;
+        }
+        j = t;
+        if (pi == cur) break;
+      }
+    }
+  }
+
+  // -- outputs: lane handles rows i = 4*lane + k ------------------------------------
+  int64_t cost = 0, dch = 0, dgh = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = 4 * lane + k;
+    const int col = c4r[k] < 0 ? 0 : c4r[k];
+    int64_t vq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vq[q] = __shfl(-nv[q], col >> 2, WAVE);
+    const int cs = col & 3;
+    const int64_t vcol = (cs == 0) ? vq[0] : (cs == 1) ? vq[1] : (cs == 2) ? vq[2] : vq[3];
+    if (i < n) {
+      const uint32_t co = own[i];
+      const int child = rows_l[i];
+      const int told = ctype[i], tnew = ctype[col];
+      if (a.flags & SH_FLAG_BUILD_ONLY) {
+        cost += single_cost(co, nw1, E);
+      } else {
+        const int64_t cij = ur[k] + vcol;  // = C[i][col] (tight matched edge)
+        const uint32_t cn = (cij == E) ? 0u : (uint32_t)((cij >> 32) + nw1);
+        cost += cij;
+        dch += child_happy(cn, nw1) - child_happy(co, nw1);
+        dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
+      }
+      if (a.col) a.col[(size_t)b * n + i] = col;
+      a.types[child] = (int16_t)tnew;  // this block owns child; ctype holds old types
+    }
+  }
+  cost = wave_sum_i64(cost);
+  dch = wave_sum_i64(dch);
+  dgh = wave_sum_i64(dgh);
+  if (lane == 0) {
+    if (a.cost) a.cost[b] = cost;
+    if (a.steps) a.steps[b] = steps;
+    if (a.delta) {
+      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
+      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
+    }
+    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generic batched LSAP.  int64 paths use the multi-wave solver (rows streamed
 // from global memory, or generated by hash); float64 uses the single-wave
 // scipy-replay solver sap_solve<K, double>.
@@ -1813,7 +2208,25 @@ struct sh_ctx {
   uint32_t *d_csr = nullptr;
   int32_t *d_err = nullptr;
   int max_lds = 0;
+  // sparse-tile kernel: LDS bytes per block (sets blocks per CU) and the
+  // double-buffered overflow lists [2 counters | 2 x ovf_cap block ids]
+  int sp_budget = 0;
+  int32_t *d_ovf = nullptr;
+  int ovf_cap = 0;
+  int ovf_par = 0;
 };
+
+namespace {
+constexpr int SP_DEFAULT_BUDGET = 160 * 1024 / 8;  // 8 blocks (waves) per CU
+
+int sp_capacity(const sh_ctx *ctx) {
+  const SpLds L0 = sp_lds_layout(ctx->ng, 0);
+  const size_t budget = (size_t)(ctx->sp_budget > 0 ? ctx->sp_budget : SP_DEFAULT_BUDGET);
+  if (budget <= L0.total) return 0;
+  const size_t cap = (budget - L0.total) / 2;
+  return (int)std::min<size_t>(cap & ~(size_t)7, 65528);
+}
+}  // namespace
 
 extern "C" {
 
@@ -1913,7 +2326,15 @@ void sh_ctx_destroy(sh_ctx *ctx) {
   if (ctx->d_csr_off) (void)hipFree(ctx->d_csr_off);
   if (ctx->d_csr) (void)hipFree(ctx->d_csr);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
+  if (ctx->d_ovf) (void)hipFree(ctx->d_ovf);
   delete ctx;
+}
+
+int sh_ctx_set_sparse_budget(sh_ctx *ctx, int bytes) {
+  if (!ctx) return fail(SH_ERR_ARGS, "null ctx");
+  if (bytes < 0 || bytes > 160 * 1024) return fail(SH_ERR_ARGS, "budget must be in [0, 160 KiB]");
+  ctx->sp_budget = bytes;
+  return sp_capacity(ctx);
 }
 
 int sh_ctx_error_flags(sh_ctx *ctx, void *stream) {
@@ -1972,6 +2393,40 @@ int launch_santa_vt(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s)
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
+
+// Sparse-tile kernel + the fallback launch for blocks whose hit lists did not
+// fit.  The two overflow counters alternate between calls: the fallback
+// launch of call k resets the counter that call k+1 appends to.
+int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
+  const int cap = sp_capacity(ctx);
+  const SpLds L = sp_lds_layout(ctx->ng, cap);
+  if (L.total > 64 * 1024) return fail(SH_ERR_ARGS, "sparse-tile LDS budget above 64 KiB");
+  if (ctx->ovf_cap < B) {
+    if (ctx->d_ovf) HIP_TRY(hipFree(ctx->d_ovf));
+    ctx->d_ovf = nullptr;
+    ctx->ovf_cap = 0;
+    const int capB = std::max(B, 4096);
+    HIP_TRY(hipMalloc(&ctx->d_ovf, (2 + 2 * (size_t)capB) * sizeof(int32_t)));
+    HIP_TRY(hipMemsetAsync(ctx->d_ovf, 0, 2 * sizeof(int32_t), s));
+    ctx->ovf_cap = capB;
+    ctx->ovf_par = 0;
+  }
+  const int p = ctx->ovf_par;
+  a.cap = cap;
+  a.ovf_cnt = ctx->d_ovf + p;
+  a.ovf_list = ctx->d_ovf + 2 + (size_t)p * ctx->ovf_cap;
+  a.blist = nullptr;
+  hipLaunchKernelGGL(santa_sp_kernel, dim3(B), dim3(WAVE), L.total, s, a);
+  HIP_TRY(hipGetLastError());
+  SantaArgs f = a;
+  f.blist = a.ovf_list;
+  f.bcount = a.ovf_cnt;
+  f.ovf_reset = ctx->d_ovf + (p ^ 1);
+  const int rc = launch_santa_vt<0>(ctx, f, B, s);
+  if (rc) return rc;
+  ctx->ovf_par = p ^ 1;
+  return SH_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -1989,6 +2444,8 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   a.steps = d_steps; a.wish = ctx->d_wish; a.csr_off = ctx->d_csr_off; a.csr = ctx->d_csr;
   a.err = ctx->d_err; a.E = ctx->E; a.n = n; a.nc = ctx->nc; a.ng = ctx->ng;
   a.n_wish = ctx->n_wish; a.n_good = ctx->n_good; a.flags = flags;
+  a.cap = 0; a.ovf_cnt = nullptr; a.ovf_list = nullptr;
+  a.blist = nullptr; a.bcount = nullptr; a.ovf_reset = nullptr;
   hipStream_t s = (hipStream_t)stream;
   if (flags & SH_FLAG_LDS_TILE)
     return mode == SH_MODE_SINGLE ? launch_santa<1, 0>(ctx, a, B, s) : launch_santa<1, 1>(ctx, a, B, s);
@@ -1996,7 +2453,8 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
   if (mode == SH_MODE_TWINS) return launch_santa<1, 1>(ctx, a, B, s);
   if (flags & SH_FLAG_SW_TILE) return launch_santa_sw(ctx, a, B, s);
-  return launch_santa_vt<0>(ctx, a, B, s);
+  if (flags & SH_FLAG_VT_TILE) return launch_santa_vt<0>(ctx, a, B, s);
+  return launch_santa_sp(ctx, a, B, s);
 }
 
 int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream) {

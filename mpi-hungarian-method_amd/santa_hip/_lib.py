@@ -23,6 +23,7 @@ SH_FLAG_EXACT_ARGMIN = 2
 SH_FLAG_BUILD_ONLY = 4
 SH_FLAG_LDS_TILE = 8
 SH_FLAG_SW_TILE = 16
+SH_FLAG_VT_TILE = 32
 SH_MAX_N = 1024
 SH_MAX_N_SANTA = 256
 
@@ -43,6 +44,7 @@ SIGNATURES = {
     "sh_score": (_I, [_P, _P, _P, _P]),
     "sh_ctx_error_flags": (_I, [_P, _P]),
     "sh_ctx_fallback_steps": (_I, [_P, _P]),
+    "sh_ctx_set_sparse_budget": (_I, [_P, _I]),
     "sh_pack_types": (_I, [_P, _P, _I, _P, _P]),
     "sh_unpack_types": (_I, [_P, _P, _I, _P, _I, _P]),
     "lsap_solve_batched_i64": (_I, [_P, _I, _I, _P, _P, _U, _P]),

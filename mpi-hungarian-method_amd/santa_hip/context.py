@@ -124,6 +124,13 @@ class SantaGPU:
     def error_flags(self) -> int:
         return _lib.check(_lib.lib().sh_ctx_error_flags(self._h, self.stream), "sh_ctx_error_flags")
 
+    def set_sparse_budget(self, nbytes: int) -> int:
+        """LDS bytes per block of the default singles kernel (0 = default);
+        returns the per-block hit-list capacity.  Blocks over it are solved by
+        the register-tile fallback launch (same results)."""
+        return _lib.check(_lib.lib().sh_ctx_set_sparse_budget(self._h, int(nbytes)),
+                          "sh_ctx_set_sparse_budget")
+
     def fallback_steps(self) -> int:
         """Steps since the last call that used the exact two-pass argmin."""
         return _lib.check(_lib.lib().sh_ctx_fallback_steps(self._h, self.stream),

@@ -306,16 +306,48 @@ def test_no_fallback_on_santa_rounds(sh, ctx, full_data):
     assert ctx.fallback_steps() == 0
 
 
+def _round_outputs(ctx, full_data, mode, rows, nn, B, fl=0):
+    types = ctx.upload_types(full_data.types)
+    col = torch.empty(B * nn, dtype=torch.int32, device="cuda")
+    cost = torch.empty(B, dtype=torch.int64, device="cuda")
+    delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+    steps = torch.empty(B, dtype=torch.int64, device="cuda")
+    ctx.solve_blocks(mode, rows, nn, types, col=col, cost=cost, delta=delta, steps=steps, flags=fl)
+    return [x.cpu().numpy() for x in (col, cost, delta, steps, types)]
+
+
+def test_sparse_overflow_fallback(sh, ctx, full_data):
+    """Blocks whose hit lists do not fit the sparse kernel's LDS budget are
+    solved by the register-tile fallback launch; any budget gives the same
+    round (all blocks overflowing, some, none), repeated calls included
+    (the double-buffered overflow counters)."""
+    from santa_hip import _lib
+    B, nn = 96, 256
+    rows = ctx.sample_blocks(0, nn, B, 5, 3)
+    want = _round_outputs(ctx, full_data, 0, rows, nn, B, _lib.SH_FLAG_VT_TILE)
+    try:
+        for budget in (6000, 16500, 17500, 0, 0, 4096, 0):
+            cap = ctx.set_sparse_budget(budget)
+            assert cap >= 0
+            got = _round_outputs(ctx, full_data, 0, rows, nn, B)
+            for x, y in zip(want, got):
+                assert np.array_equal(x, y), budget
+        assert ctx.error_flags() == 0
+    finally:
+        ctx.set_sparse_budget(0)
+
+
 def test_kernel_designs_agree(sh, ctx, full_data):
-    """The 4-wave register-tile kernel (default for singles), the one-wave
-    register kernel (SH_FLAG_SW_TILE) and the 4-wave LDS-tile kernel
-    (SH_FLAG_LDS_TILE) produce identical rounds: col, cost, deltas, steps, state."""
+    """The one-wave sparse-tile kernel (default for singles), the 4-wave
+    register-tile kernel (SH_FLAG_VT_TILE), the one-wave register kernel
+    (SH_FLAG_SW_TILE) and the 4-wave LDS-tile kernel (SH_FLAG_LDS_TILE)
+    produce identical rounds: col, cost, deltas, steps, state."""
     from santa_hip import _lib
     mode = 0
-    for B, nn in ((64, 256), (16, 100), (8, 37), (8, 130), (4, 1)):
+    for B, nn in ((64, 256), (16, 100), (8, 37), (8, 130), (4, 1), (6, 255), (5, 64)):
         rows = ctx.sample_blocks(mode, nn, B, 77, 9)
         outs = []
-        for fl in (0, _lib.SH_FLAG_SW_TILE, _lib.SH_FLAG_LDS_TILE):
+        for fl in (0, _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_SW_TILE, _lib.SH_FLAG_LDS_TILE):
             types = ctx.upload_types(full_data.types)
             col = torch.empty(B * nn, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")
