@@ -1575,13 +1575,17 @@ __global__ __launch_bounds__(WAVE, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 // per-row hit lists of (column, code) uint16 entries, ~26 per row on
 // Kaggle-shaped data (~13 KB per block).  A Dijkstra step expands row i into
 // a 256-byte LDS row buffer (one ds_write_b8 per hit); each lane reads the
-// dword holding its four codes and clears it.  Everything else a step
-// touches is in registers: spc / -v / path / position / key bits per owned
-// column, the row duals u~ and the rows' hit ranges per owned row (the u~
-// bookkeeping of santa_vt_kernel: u~[i] -= m when row i is reached, += the
-// final minimum for visited rows).  ~20 KB LDS per block -> 8 blocks per CU,
-// i.e. two waves per SIMD hiding each other's LDS and DPP latencies, with
-// about a third of the register-tile kernel's VALU work per Dijkstra step.
+// dword holding its four codes and clears it.
+// Per column the step keeps, in VGPRs: sb = spc + BIAS (every Dijkstra starts
+// at minVal = 0, so the packed argmin key is read straight off sb), W = -v,
+// path and the key's tie-break bits lo; the live (still `remaining`) columns
+// are wave masks in SGPRs.  scipy's `remaining` array itself is in LDS
+// (uint8 per position), so the one column that moves per step is updated by
+// one lane.  Row duals u are in LDS (one broadcast ds_read_b64 per step);
+// rows reached in the current Dijkstra are listed so that scipy's dual update
+// (u[i] += minVal - spc[col4row[i]]) runs once at the end of the Dijkstra,
+// using u~[i] = u[i] - (minVal when row i was reached) during it.
+// ~20 KB LDS per block -> 8 blocks per CU (two waves per SIMD).
 // A block whose hit lists overflow the LDS capacity is left untouched and
 // appended to an overflow list; santa_vt_kernel (register tile, any hit
 // count) solves those in a second launch.  Decisions are scipy's, as in
@@ -1590,20 +1594,31 @@ __global__ __launch_bounds__(WAVE, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 constexpr int SP_UMAX = 4;  // wishlist chunks per lane per build group
 
 struct SpLds {
-  size_t rowbuf, rows, ctype, nxt, own, gcnt, off, head, hits, total;
+  // persistent
+  size_t rowbuf, ctype, own, hits;
+  // build phase                      // solve phase (aliases the build area)
+  size_t rows, head, nxt, gcnt, off;  size_t u, rem, vrow;
+  size_t total;
 };
 
 __host__ __device__ __forceinline__ SpLds sp_lds_layout(int ng, int cap) {
   SpLds L;
   size_t o = 0;
   L.rowbuf = o; o += 256;                // row buffer: code of column j at byte j
-  L.rows = o;   o += 256 * 4;            // child ids
   L.ctype = o;  o += 256 * 2;            // column gift types (old)
-  L.nxt = o;    o += 256 * 2;            // type -> column chains
   L.own = o;    o += 256;                // code(i, i): row i's own (old) gift
-  L.gcnt = o;   o += 64 * 4;             // per-row hit counters of a build group
-  L.off = o;    o += r16(257 * 2);       // hit-list offsets per row
-  L.head = o;   o += r16((size_t)((ng + 1) / 2) * 4);  // int16 chain heads
+  const size_t area = o;
+  size_t b = area;                       // build phase
+  L.rows = b;   b += 256 * 4;            // child ids
+  L.nxt = b;    b += 256 * 2;            // type -> column chains
+  L.gcnt = b;   b += 64 * 4;             // per-row hit counters of a build group
+  L.off = b;    b += r16(257 * 2);       // hit-list offsets per row
+  L.head = b;   b += r16((size_t)((ng + 1) / 2) * 4);  // int16 chain heads
+  size_t s = area;                       // solve phase
+  L.u = s;      s += 256 * 8;            // row duals
+  L.rem = s;    s += 256;                // scipy's `remaining`: column at position p
+  L.vrow = s;   s += 256;                // rows reached in the current Dijkstra
+  o = b > s ? b : s;
   L.hits = o;   o += r16((size_t)cap * 2);
   L.total = o;
   return L;
@@ -1636,6 +1651,13 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
   return x;
 }
 
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint64_t rfl_u64(uint64_t x) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+
 __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
@@ -1645,14 +1667,17 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   const SpLds L = sp_lds_layout(a.ng, cap);
   uint8_t *rowbuf = smem + L.rowbuf;
   uint32_t *rowbuf32 = (uint32_t *)(smem + L.rowbuf);
-  int32_t *rows_l = (int32_t *)(smem + L.rows);
   int16_t *ctype = (int16_t *)(smem + L.ctype);
-  int16_t *nxt = (int16_t *)(smem + L.nxt);
   uint8_t *own = smem + L.own;
+  uint16_t *hits = (uint16_t *)(smem + L.hits);
+  int32_t *rows_l = (int32_t *)(smem + L.rows);
+  int16_t *nxt = (int16_t *)(smem + L.nxt);
   uint32_t *gcnt = (uint32_t *)(smem + L.gcnt);
   uint16_t *off = (uint16_t *)(smem + L.off);
   uint32_t *head32 = (uint32_t *)(smem + L.head);
-  uint16_t *hits = (uint16_t *)(smem + L.hits);
+  int64_t *u_l = (int64_t *)(smem + L.u);
+  uint8_t *rem = smem + L.rem;
+  uint8_t *vrow = smem + L.vrow;
 
   // -- rows, range check, chains ------------------------------------------------
   int bad = 0;
@@ -1759,25 +1784,28 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   }
   if (lane == 0) off[n] = (uint16_t)base;
   __syncthreads();
-  uint32_t offr[4];  // hit range of row 4*lane + k: start | end << 16
+  i32x4 offr;  // hit range of row 4*lane + k: start | end << 16
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int r = 4 * lane + k;
-    offr[k] = (r < n) ? ((uint32_t)off[r] | ((uint32_t)off[r + 1] << 16)) : 0u;
+    offr[k] = (r < n) ? (int)((uint32_t)off[r] | ((uint32_t)off[r + 1] << 16)) : 0;
   }
+  __syncthreads();  // the build area becomes the solve area (u, rem, vrow)
+  for (int r = lane; r < n; r += WAVE) u_l[r] = 0;
 
   // -- solve ----------------------------------------------------------------------
   const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
-  const int64_t INF = INT64_MAX;
   const int64_t E = a.E;
-  int64_t spc[4], nv[4], ur[4];  // nv = -v of owned columns; ur = u~ of owned rows
-  int path[4], pos[4], r4c[4], c4r[4];
+  uint32_t Ev = (uint32_t)E;
+  asm volatile("" : "+v"(Ev));  // the miss value as a VGPR constant
+  const uint64_t BIAS = (uint64_t)KEY_BIAS;
+  int64_t sb[4], W[4];  // spc + BIAS; -v   (columns 4*lane + k)
+  i32x4 path, r4c, c4r;
   uint32_t lo[4];
-  bool live[4];
+  uint64_t LM[4];       // live (remaining) columns, wave masks
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    nv[k] = 0;
-    ur[k] = 0;
+    W[k] = 0;
     path[k] = -1;
     r4c[k] = -1;
     c4r[k] = -1;
@@ -1789,73 +1817,90 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     for (int k = 0; k < 4; ++k) c4r[k] = r4c[k] = 4 * lane + k;
   } else {
     for (int cur = 0; cur < n; ++cur) {
+      // Dijkstra set-up: remaining = [n-1 .. 0], all columns live
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int j = 4 * lane + k;
-        spc[k] = INF;
-        live[k] = j < n;
-        pos[k] = n - 1 - j;
-        lo[k] = (r4c[k] < 0) ? (((uint32_t)(1023 - pos[k]) << 10) | (uint32_t)j)
-                             : ((1u << 20) | ((uint32_t)pos[k] << 10) | (uint32_t)r4c[k]);
+        const int pos = n - 1 - j;
+        sb[k] = INT64_MAX;
+        lo[k] = (r4c[k] < 0) ? (((uint32_t)(1023 - pos) << 10) | (uint32_t)j)
+                             : ((1u << 20) | ((uint32_t)pos << 10) | (uint32_t)r4c[k]);
+        LM[k] = __builtin_amdgcn_ballot_w64(j < n);
       }
-      uint32_t vis = ((cur >> 2) == lane) ? (1u << (cur & 3)) : 0u;
+      {
+        uint32_t rw = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rw |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
+        ((uint32_t *)rem)[lane] = rw;  // rem[p] = n - 1 - p
+      }
+      if (lane == 0) vrow[0] = (uint8_t)cur;
+      int nvis = 1;
       int nrem = n;
       int64_t minVal = 0;
       int i = cur;
       int sink;
+      int mover = __builtin_amdgcn_readfirstlane((int)rem[n - 1]);  // column at the last position
       for (;;) {
         ++steps;
-        const int64_t ui = readlane_i64(pick4(ur, i & 3), i >> 2);
-        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)pick4(offr, i & 3), i >> 2);
-        // expand row i into the row buffer, read this lane's four codes, clear
-        for (int s = (int)(o & 0xFFFFu) + lane; s < (int)(o >> 16); s += WAVE) {
-          const uint32_t e = hits[s];
+        // row i: hit range (registers), dual u[i] (LDS broadcast)
+        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane(offr[i & 3], i >> 2);
+        const int hs = (int)(o & 0xFFFFu), he = (int)(o >> 16);
+        const uint64_t uraw = (uint64_t)u_l[i];
+        if (hs + lane < he) {
+          const uint32_t e = hits[hs + lane];
           rowbuf[e & 0xFFu] = (uint8_t)(e >> 8);
+        }
+        if (__builtin_expect(he - hs > WAVE, 0)) {  // rows with more than 64 hits
+          for (int s = hs + WAVE + lane; s < he; s += WAVE) {
+            const uint32_t e = hits[s];
+            rowbuf[e & 0xFFu] = (uint8_t)(e >> 8);
+          }
         }
         const uint32_t w = rowbuf32[lane];
         rowbuf32[lane] = 0;
-        // r = C[i][j] - u~[i] - v[j]:  C = code ? (code - nw1) * 2^32 : E
-        const uint64_t a1 = (uint64_t)(-ui);      // hit:  -u~ + (code - nw1) << 32
-        const uint64_t a0 = (uint64_t)(E - ui);   // miss: E - u~
-        const uint64_t kb = (uint64_t)KEY_BIAS - (uint64_t)minVal;
+        // u~[i] = u[i] - (minVal at which row i was reached) = u[i] - minVal now
+        const int64_t ui = (int64_t)rfl_u64(uraw) - minVal;
+        if (lane == 0) u_l[i] = ui;
+        // r + BIAS = C[i][j] - u~[i] - v[j] + BIAS;  C = code ? (code - nw1) << 32 : E
+        uint64_t bse = BIAS - (uint64_t)ui;
+        asm volatile("" : "+s"(bse));  // keep W + bse one 64-bit add
         uint64_t best = ~0ull;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const uint32_t code = (w >> (8 * k)) & 0xFFu;
-          const uint32_t tl = code ? (uint32_t)a1 : (uint32_t)a0;
-          const uint32_t th = code ? (uint32_t)(a1 >> 32) + code - (uint32_t)nw1 : (uint32_t)(a0 >> 32);
-          const int64_t r = nv[k] + (int64_t)(((uint64_t)th << 32) | tl);
-          const bool upd = live[k] && (r < spc[k]);
-          spc[k] = upd ? r : spc[k];
+          const uint64_t hit = code ? ((uint64_t)(code - (uint32_t)nw1) << 32) : (uint64_t)Ev;
+          const uint64_t r = ((uint64_t)W[k] + bse) + hit;
+          const bool lv = __builtin_amdgcn_inverse_ballot_w64(LM[k]);
+          const bool upd = lv && ((int64_t)r < sb[k]);
+          sb[k] = upd ? (int64_t)r : sb[k];
           path[k] = upd ? i : path[k];
-          const uint64_t sb = (uint64_t)spc[k] + kb;
-          const uint32_t sh = (uint32_t)(sb >> 32), sl = (uint32_t)sb;
-          uint32_t kh = __builtin_amdgcn_alignbit(sh, sl, 11);
-          kh = (sh < 2048u) ? kh : ((int32_t)sh < 0 ? 0u : 0xFFFFFFFFu);
+          const uint32_t sh = (uint32_t)((uint64_t)sb[k] >> 32), sl = (uint32_t)sb[k];
+          // bits 11..42 of sb, saturated to all-ones from 2^43 (sb > 0 here:
+          // spc >= min C - v >= -n_wish * 2^32 > -BIAS)
+          const uint32_t sat = (uint32_t)((int32_t)(2047u - sh) >> 31);
+          const uint32_t kh = __builtin_amdgcn_alignbit(sh, sl, 11) | sat;
           const uint64_t key = ((uint64_t)kh << 32) | ((sl << 21) | lo[k]);
-          best = (live[k] && key < best) ? key : best;
+          best = (lv && key < best) ? key : best;
         }
-        uint64_t g = wave_min_u64_fast(best);
-        g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
-            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+        uint64_t g = rfl_u64(wave_min_u64_fast(best));
         const uint32_t ghi = (uint32_t)(g >> 32);
-        if (exact || ghi == 0u || ghi == 0xFFFFFFFFu) {
+        if (exact || ghi + 1u <= 1u) {  // saturated key (ghi 0 or ~0)
+          // exact two-pass argmin: min sb (signed), then min tie-break bits
           uint64_t m = ~0ull;
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            if (live[k]) m = umin64(m, (uint64_t)spc[k] ^ SIGN64);
+            if (__builtin_amdgcn_inverse_ballot_w64(LM[k])) m = umin64(m, (uint64_t)sb[k] ^ SIGN64);
           m = wave_min_u64_dpp(m);
           const int64_t ms = (int64_t)(m ^ SIGN64);
           uint64_t b2 = ~0ull;
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            if (live[k] && spc[k] == ms) b2 = umin64(b2, (uint64_t)lo[k]);
-          g = wave_min_u64_dpp(b2);
-          g = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
-          minVal = ms;
+            if (__builtin_amdgcn_inverse_ballot_w64(LM[k]) && sb[k] == ms) b2 = umin64(b2, (uint64_t)lo[k]);
+          g = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wave_min_u64_dpp(b2));
+          minVal = (int64_t)((uint64_t)ms - BIAS);
           ++fallbacks;
         } else {
-          minVal = minVal + ((int64_t)(g >> KEY_LO_BITS) - KEY_BIAS);
+          minVal = (int64_t)((g >> KEY_LO_BITS) - BIAS);
         }
         const uint32_t glo = (uint32_t)g & 0x1FFFFFu;
         const bool assigned = (glo >> 20) & 1u;
@@ -1863,47 +1908,51 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         const int aux = (int)(glo & 1023u);
         const int pstar = assigned ? pk : 1023 - pk;
         const int last = nrem - 1;
-        const uint32_t X = (uint32_t)(last ^ pstar) << 10;
+        // the winner leaves `remaining`; the column at `last` moves to pstar
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          live[k] = live[k] && (lo[k] != glo);
-          const bool mv = pos[k] == last;
-          pos[k] = mv ? pstar : pos[k];
-          lo[k] = mv ? (lo[k] ^ X) : lo[k];
+        for (int k = 0; k < 4; ++k) LM[k] &= ~__builtin_amdgcn_ballot_w64(lo[k] == glo);
+        if (pstar != last) {
+          const uint32_t X = (uint32_t)(last ^ pstar) << 10;
+          if (lane == 0) rem[pstar] = (uint8_t)mover;
+          const int mk = mover & 3;
+          const uint32_t Xl = (lane == (mover >> 2)) ? X : 0u;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) lo[k] ^= (mk == k) ? Xl : 0u;
         }
         --nrem;
         if (!assigned) {
           sink = aux;
           break;
         }
+        mover = __builtin_amdgcn_readfirstlane((int)rem[last - 1]);
         i = __builtin_amdgcn_readfirstlane(aux);
-        if ((i >> 2) == lane) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if ((i & 3) == k) ur[k] -= minVal;
-        }
-        vis |= ((i >> 2) == lane) ? (1u << (i & 3)) : 0u;
+        if (lane == 0) vrow[nvis] = (uint8_t)i;
+        ++nvis;
       }
+      // dual updates: visited columns v[j] -= minVal - spc[j]; visited rows
+      // u[i] = u~[i] + minVal (= u[i] + minVal - spc[col4row[i]])
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if ((vis >> k) & 1u) ur[k] += minVal;
-        if (4 * lane + k < n && !live[k]) nv[k] = nv[k] + (minVal - spc[k]);
+        const bool visited = (4 * lane + k < n) && !((LM[k] >> lane) & 1ull);
+        if (visited) W[k] = W[k] + (minVal - (int64_t)((uint64_t)sb[k] - BIAS));
+      }
+      for (int t = lane; t < nvis; t += WAVE) {
+        const int r = vrow[t];
+        u_l[r] = u_l[r] + minVal;
       }
       // augment along path[] from the sink back to cur (registers only)
       int j = sink;
       for (;;) {
-        const int pi = __builtin_amdgcn_readlane(pick4(path, j & 3), j >> 2);
-        const int t = __builtin_amdgcn_readlane(pick4(c4r, pi & 3), pi >> 2);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (4 * lane + k == j) r4c[k] = pi;
-          if (4 * lane + k == pi) c4r[k] = j;
-        }
+        const int pi = __builtin_amdgcn_readlane(path[j & 3], j >> 2);
+        const int t = __builtin_amdgcn_readlane(c4r[pi & 3], pi >> 2);
+        if (lane == (j >> 2)) r4c[j & 3] = pi;
+        if (lane == (pi >> 2)) c4r[pi & 3] = j;
         j = t;
         if (pi == cur) break;
       }
     }
   }
+  __syncthreads();
 
   // -- outputs: lane handles rows i = 4*lane + k ------------------------------------
   int64_t cost = 0, dch = 0, dgh = 0;
@@ -1913,17 +1962,17 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     const int col = c4r[k] < 0 ? 0 : c4r[k];
     int64_t vq[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) vq[q] = __shfl(-nv[q], col >> 2, WAVE);
+    for (int q = 0; q < 4; ++q) vq[q] = __shfl(-W[q], col >> 2, WAVE);
     const int cs = col & 3;
     const int64_t vcol = (cs == 0) ? vq[0] : (cs == 1) ? vq[1] : (cs == 2) ? vq[2] : vq[3];
     if (i < n) {
       const uint32_t co = own[i];
-      const int child = rows_l[i];
+      const int child = a.rows[(size_t)b * n + i];
       const int told = ctype[i], tnew = ctype[col];
       if (a.flags & SH_FLAG_BUILD_ONLY) {
         cost += single_cost(co, nw1, E);
       } else {
-        const int64_t cij = ur[k] + vcol;  // = C[i][col] (tight matched edge)
+        const int64_t cij = u_l[i] + vcol;  // = C[i][col] (tight matched edge)
         const uint32_t cn = (cij == E) ? 0u : (uint32_t)((cij >> 32) + nw1);
         cost += cij;
         dch += child_happy(cn, nw1) - child_happy(co, nw1);

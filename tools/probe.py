@@ -23,9 +23,11 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--phase", choices=["all", "build", "solve", "score"], default="all")
     ap.add_argument("--flags", type=int, default=0, help="extra SH_FLAG_* bits (8 = LDS tile)")
+    ap.add_argument("--budget", type=int, default=0, help="sparse kernel LDS bytes per block (0 = default)")
     a = ap.parse_args()
     sd = D.synthetic(2017)
     ctx = SantaGPU.from_data(sd, 0)
+    cap = ctx.set_sparse_budget(a.budget)
     _, _, _, nb = ctx.geometry(a.mode, a.n)
     B = a.blocks or nb
     rows = ctx.sample_blocks(a.mode, a.n, B, 2017, 0)
@@ -56,6 +58,9 @@ def main():
             ts.append(e0.elapsed_time(e1))
         out["score"] = {"ms": min(ts), "all_ms": ts}
     out["blocks"] = B
+    out["budget"] = a.budget
+    out["cap"] = cap
+    out["flags"] = a.flags
     out["steps_total"] = int(steps.sum())
     out["steps_per_block"] = int(steps.sum()) / B
     print(json.dumps(out))
