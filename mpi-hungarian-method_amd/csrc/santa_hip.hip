@@ -1774,8 +1774,9 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         for (int z = 0; z < 4; ++z) {
           if (z < wpc) {
             const int g = (int)(int16_t)(((z < 2 ? q[u].x : q[u].y) >> (16 * (z & 1))) & 0xFFFFu);
-            const uint32_t code = (uint32_t)(cc * wpc + z + 1) << 8;
-            for (int jj = head_get(head32, g); jj >= 0; jj = nxt[jj]) hits[p++] = (uint16_t)(code | (uint32_t)jj);
+            // the tile byte is code - (n_wish + 1), a negative int8 (0 = miss)
+            const uint32_t tb = ((uint32_t)(cc * wpc + z - nw) & 0xFFu) << 8;
+            for (int jj = head_get(head32, g); jj >= 0; jj = nxt[jj]) hits[p++] = (uint16_t)(tb | (uint32_t)jj);
           }
         }
       }
@@ -1867,24 +1868,24 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         uint64_t best = ~0ull;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const uint32_t code = (w >> (8 * k)) & 0xFFu;
-          const uint64_t hit = code ? ((uint64_t)(code - (uint32_t)nw1) << 32) : (uint64_t)Ev;
+          const int32_t tb = (int32_t)(int8_t)((w >> (8 * k)) & 0xFFu);  // code - nw1, 0 = miss
+          const uint64_t hit = tb ? ((uint64_t)(uint32_t)tb << 32) : (uint64_t)Ev;
           const uint64_t r = ((uint64_t)W[k] + bse) + hit;
           const bool lv = __builtin_amdgcn_inverse_ballot_w64(LM[k]);
           const bool upd = lv && ((int64_t)r < sb[k]);
           sb[k] = upd ? (int64_t)r : sb[k];
           path[k] = upd ? i : path[k];
           const uint32_t sh = (uint32_t)((uint64_t)sb[k] >> 32), sl = (uint32_t)sb[k];
-          // bits 11..42 of sb, saturated to all-ones from 2^43 (sb > 0 here:
-          // spc >= min C - v >= -n_wish * 2^32 > -BIAS)
-          const uint32_t sat = (uint32_t)((int32_t)(2047u - sh) >> 31);
-          const uint32_t kh = __builtin_amdgcn_alignbit(sh, sl, 11) | sat;
+          // bits 11..42 of sb (sb > 0 here: spc >= min C - v >= -n_wish * 2^32
+          // > -BIAS); from sb >= 2047 * 2^32 the key saturates at >= 0xFFE00000
+          // and a saturated winner is re-decided by the exact argmin below
+          const uint32_t kh = __builtin_amdgcn_alignbit(min(sh, 2047u), sl, 11);
           const uint64_t key = ((uint64_t)kh << 32) | ((sl << 21) | lo[k]);
           best = (lv && key < best) ? key : best;
         }
         uint64_t g = rfl_u64(wave_min_u64_fast(best));
         const uint32_t ghi = (uint32_t)(g >> 32);
-        if (exact || ghi + 1u <= 1u) {  // saturated key (ghi 0 or ~0)
+        if (exact || ghi - 1u >= 0xFFDFFFFFu) {  // saturated key (0, or >= 0xFFE00000)
           // exact two-pass argmin: min sb (signed), then min tie-break bits
           uint64_t m = ~0ull;
 #pragma unroll

@@ -24,14 +24,18 @@ def main():
     ap.add_argument("--phase", choices=["all", "build", "solve", "score"], default="all")
     ap.add_argument("--flags", type=int, default=0, help="extra SH_FLAG_* bits (8 = LDS tile)")
     ap.add_argument("--budget", type=int, default=0, help="sparse kernel LDS bytes per block (0 = default)")
+    ap.add_argument("--state-round", type=int, default=0,
+                    help="time round R of the optimisation: first apply rounds 0..R-1 (default kernel)")
     a = ap.parse_args()
     sd = D.synthetic(2017)
     ctx = SantaGPU.from_data(sd, 0)
     cap = ctx.set_sparse_budget(a.budget)
     _, _, _, nb = ctx.geometry(a.mode, a.n)
     B = a.blocks or nb
-    rows = ctx.sample_blocks(a.mode, a.n, B, 2017, 0)
     base = ctx.upload_types(sd.types)
+    for r in range(a.state_round):
+        ctx.solve_blocks(a.mode, ctx.sample_blocks(a.mode, a.n, nb, 2017, r), a.n, base)
+    rows = ctx.sample_blocks(a.mode, a.n, B, 2017, a.state_round)
     steps = torch.empty(B, dtype=torch.int64, device="cuda")
     out = {}
     for name, fl in (("build", _lib.SH_FLAG_BUILD_ONLY), ("solve", 0)):
@@ -61,6 +65,7 @@ def main():
     out["budget"] = a.budget
     out["cap"] = cap
     out["flags"] = a.flags
+    out["state_round"] = a.state_round
     out["steps_total"] = int(steps.sum())
     out["steps_per_block"] = int(steps.sum()) / B
     print(json.dumps(out))
