@@ -45,13 +45,16 @@ extern "C" {
 #define SH_FLAG_EXACT_ARGMIN 2u /* always use the two-pass exact argmin    */
 #define SH_FLAG_BUILD_ONLY 4u   /* sh_solve_blocks: build the cost tiles and
                                    apply the identity (phase timing only)  */
-#define SH_FLAG_LDS_TILE 8u     /* sh_solve_blocks, singles n <= 256:       */
-#define SH_FLAG_SW_TILE 16u     /* alternative kernel designs (4-wave LDS   */
+#define SH_FLAG_LDS_TILE 8u     /* sh_solve_blocks, singles n <= 256:      */
+#define SH_FLAG_SW_TILE 16u     /* alternative kernel designs (4-wave LDS  */
 #define SH_FLAG_VT_TILE 32u     /* tile / one-wave register tile / 4-wave
                                    register tile) kept for A/B profiling;
                                    identical results.  Default: one-wave
                                    sparse LDS tile (+ register-tile fallback
                                    for blocks whose hit lists overflow)    */
+#define SH_FLAG_TIMING 64u      /* dev: the sparse kernel writes phase times
+                                   (wall-clock ticks since its start, 3 x 21
+                                   bits: built, solved, done) into d_steps */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024

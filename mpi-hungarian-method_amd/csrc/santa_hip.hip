@@ -1591,13 +1591,12 @@ __global__ __launch_bounds__(WAVE, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 // count) solves those in a second launch.  Decisions are scipy's, as in
 // every other kernel here.
 // ---------------------------------------------------------------------------
-constexpr int SP_UMAX = 4;  // wishlist chunks per lane per build group
 
 struct SpLds {
   // persistent
   size_t rowbuf, ctype, own, hits;
-  // build phase                      // solve phase (aliases the build area)
-  size_t rows, head, nxt, gcnt, off;  size_t u, rem, vrow;
+  // build phase                // solve phase (aliases the build area)
+  size_t csort, thead, off;     size_t u, rem, vrow;
   size_t total;
 };
 
@@ -1609,36 +1608,18 @@ __host__ __device__ __forceinline__ SpLds sp_lds_layout(int ng, int cap) {
   L.own = o;    o += 256;                // code(i, i): row i's own (old) gift
   const size_t area = o;
   size_t b = area;                       // build phase
-  L.rows = b;   b += 256 * 4;            // child ids
-  L.nxt = b;    b += 256 * 2;            // type -> column chains
-  L.gcnt = b;   b += 64 * 4;             // per-row hit counters of a build group
+  L.csort = b;  b += 272;                // columns sorted by gift type (+ pad)
+  L.thead = b;  b += r16((size_t)ng * 2);  // per type: start in csort | count << 8
   L.off = b;    b += r16(257 * 2);       // hit-list offsets per row
-  L.head = b;   b += r16((size_t)((ng + 1) / 2) * 4);  // int16 chain heads
   size_t s = area;                       // solve phase
   L.u = s;      s += 256 * 8;            // row duals
   L.rem = s;    s += 256;                // scipy's `remaining`: column at position p
   L.vrow = s;   s += 256;                // rows reached in the current Dijkstra
   o = b > s ? b : s;
-  L.hits = o;   o += r16((size_t)cap * 2);
+  L.hits = o;   // + a dump dword per lane; also the counting-sort scratch (ng x u32)
+  o += r16(std::max((size_t)(cap + 2 * 64) * 2, (size_t)ng * 4));
   L.total = o;
   return L;
-}
-
-// head[t] <- j, returns the previous head (int16 heads, two per dword).
-__device__ __forceinline__ int head_push(uint32_t *head32, int t, int j) {
-  uint32_t *w = head32 + (t >> 1);
-  const int sh = (t & 1) * 16;
-  uint32_t old = *w, assumed;
-  do {
-    assumed = old;
-    const uint32_t nw = (assumed & ~(0xFFFFu << sh)) | ((uint32_t)(uint16_t)j << sh);
-    old = atomicCAS(w, assumed, nw);
-  } while (old != assumed);
-  return (int)(int16_t)((assumed >> sh) & 0xFFFFu);
-}
-
-__device__ __forceinline__ int head_get(const uint32_t *head32, int t) {
-  return (int)(int16_t)((head32[t >> 1] >> ((t & 1) * 16)) & 0xFFFFu);
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
@@ -1658,6 +1639,7 @@ __device__ __forceinline__ uint64_t rfl_u64(uint64_t x) {
          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
 }
 
+template <bool VEC>
 __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
@@ -1670,118 +1652,213 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   int16_t *ctype = (int16_t *)(smem + L.ctype);
   uint8_t *own = smem + L.own;
   uint16_t *hits = (uint16_t *)(smem + L.hits);
-  int32_t *rows_l = (int32_t *)(smem + L.rows);
-  int16_t *nxt = (int16_t *)(smem + L.nxt);
-  uint32_t *gcnt = (uint32_t *)(smem + L.gcnt);
+  uint8_t *csort = smem + L.csort;
+  uint16_t *thead = (uint16_t *)(smem + L.thead);
   uint16_t *off = (uint16_t *)(smem + L.off);
-  uint32_t *head32 = (uint32_t *)(smem + L.head);
+  uint32_t *tcnt = (uint32_t *)(smem + L.hits);  // counting-sort scratch (hits not yet built)
   int64_t *u_l = (int64_t *)(smem + L.u);
   uint8_t *rem = smem + L.rem;
   uint8_t *vrow = smem + L.vrow;
 
-  // -- rows, range check, chains ------------------------------------------------
+  const uint64_t t0 = (a.flags & SH_FLAG_TIMING) ? wall_clock64() : 0;
+  // -- rows (lane l owns rows 4l..4l+3), range check --------------------------------
+  int child[4];
   int bad = 0;
-  for (int j = lane; j < n; j += WAVE) {
-    const int r = a.rows[(size_t)b * n + j];
-    bad |= (r < 0) || (r >= a.nc);
-    rows_l[j] = r;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = 4 * lane + k;
+    child[k] = (r < n) ? a.rows[(size_t)b * n + r] : 0;
+    bad |= (r < n) && ((child[k] < 0) || (child[k] >= a.nc));
   }
   if (__any(bad)) {
     if (lane == 0) atomicOr(a.err, 1);
     return;
   }
-  for (int t = lane; t < (a.ng + 1) / 2; t += WAVE) head32[t] = 0xFFFFFFFFu;
+  // Warm the TLB and L2 with the block's 256 wishlist rows (random children,
+  // one page each) while the column sort runs: three dword loads per row.
+  uint32_t warm[4][3];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t *src = (const uint32_t *)(a.wish + (size_t)child[k] * a.n_wish);
+    const int last = (a.n_wish * 2 - 4) >> 2;  // last whole dword of the row
+#pragma unroll
+    for (int x = 0; x < 3; ++x) warm[k][x] = src[min(x * 24, last)];
+  }
+  // -- columns sorted by gift type (counting sort; order within a type is free)
+  // u32 counters in the (still empty) hit-list area, then a u16 table per
+  // type: start in csort | count << 8.  A type with >= 255 columns in one
+  // block (never on Kaggle-shaped data) sends the block to the fallback.
+  for (int t = lane; t < a.ng; t += WAVE) tcnt[t] = 0u;
   rowbuf32[lane] = 0;
   ((uint32_t *)own)[lane] = 0;
-  gcnt[lane] = 0;
+  int myt[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) myt[k] = (4 * lane + k < n) ? a.types[child[k]] : -1;
   __syncthreads();
-  for (int j = lane; j < n; j += WAVE) {
-    const int ty = a.types[rows_l[j]];
-    ctype[j] = (int16_t)ty;
-    nxt[j] = (int16_t)head_push(head32, ty, j);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (myt[k] >= 0) {
+      ctype[4 * lane + k] = (int16_t)myt[k];
+      atomicAdd(&tcnt[myt[k]], 1u << 16);
+    }
   }
   __syncthreads();
+  int big = 0;
+  {  // exclusive scan of the counts over types -> start of each type in csort
+    const int per = (a.ng + WAVE - 1) / WAVE;
+    const int t0s = lane * per, t1s = min(a.ng, t0s + per);
+    uint32_t sum = 0;
+    for (int t = t0s; t < t1s; ++t) sum += tcnt[t] >> 16;
+    uint32_t run = wave_incl_scan_u32(sum) - sum;
+    for (int t = t0s; t < t1s; ++t) {
+      const uint32_t h = tcnt[t];
+      tcnt[t] = h | run;  // low half: fill cursor
+      big |= (h >> 16) >= 255u;
+      thead[t] = (h >> 16) ? (uint16_t)(run | ((h >> 16) << 8)) : (uint16_t)0;  // start < 256 if present
+      run += h >> 16;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (myt[k] >= 0) csort[atomicAdd(&tcnt[myt[k]], 1u) & 0xFFFFu] = (uint8_t)(4 * lane + k);
+  __syncthreads();
+  const uint64_t tc = (a.flags & SH_FLAG_TIMING) ? wall_clock64() : 0;
 
-  // -- build the hit lists, G rows at a time ---------------------------------------
-  // chunk = 4 wishes (8-byte load) when n_wish % 4 == 0, else 1 wish.
+  // -- hit lists, 8 rows per sub-round, 8 lanes per row ------------------------------
+  // Row i's entries are (column, code - (n_wish+1)) for every column whose gift
+  // type child i wishes.  Lane 8q+j takes chunks [j*ncq, (j+1)*ncq) (4 wishes
+  // per chunk) of row s0+q: the 8 rows' wishlists are read 64 lanes at a
+  // time (TLB-friendly), counted from the per-type column counts, placed by
+  // one wave scan (row-major lanes = contiguous rows), then filled branch-free
+  // (surplus writes go to the lane's dump slot).
   const int nw = a.n_wish;
   const int nw1 = nw + 1;
-  const bool vec = (nw & 3) == 0;
-  const int cpr = vec ? (nw >> 2) : nw;          // chunks per row
-  const int wpc = vec ? 4 : 1;                   // wishes per chunk
-  const int G = min(64, max(1, (WAVE * SP_UMAX) / cpr));
+  constexpr int LPR = 8;                         // lanes per row
+  constexpr int RPS = WAVE / LPR;                // rows per sub-round
+  constexpr int MAXQ = 4;                        // chunks per lane (n_wish <= 127)
+  const int nch = (nw + 3) >> 2;
+  const int ncq = (nch + LPR - 1) / LPR;
+  const int qr = lane / LPR, qj = lane % LPR;
   int base = 0;
-  for (int r0 = 0; r0 < n; r0 += G) {
-    const int grows = min(G, n - r0);
-    const int gch = grows * cpr;
-    uint2 q[SP_UMAX];
-    int slot[SP_UMAX];
+  bool fits = !__any(big);
+  auto load_chunk = [&](const int16_t *src, int c) -> uint2 {
+    uint2 q;
+    if constexpr (VEC) {
+      q = *(const uint2 *)(src + 4 * min(c, nch - 1));
+    } else {
+      uint32_t g4[4];
 #pragma unroll
-    for (int u = 0; u < SP_UMAX; ++u) {
-      const int c = lane + WAVE * u;
-      if (c < gch) {
-        const int row = r0 + c / cpr, cc = c - (c / cpr) * cpr;
-        const int16_t *src = a.wish + (size_t)rows_l[row] * nw;
-        if (vec) {
-          q[u] = *(const uint2 *)(src + 4 * cc);
-        } else {
-          q[u].x = (uint32_t)(uint16_t)src[cc] | 0xFFFF0000u;
-          q[u].y = 0xFFFFFFFFu;
-        }
+      for (int z = 0; z < 4; ++z) {
+        const int r = 4 * c + z;
+        g4[z] = (r < nw) ? (uint16_t)src[min(r, nw - 1)] : 0xFFFFu;
+      }
+      q.x = g4[0] | (g4[1] << 16);
+      q.y = g4[2] | (g4[3] << 16);
+    }
+    return q;
+  };
+  auto gift_of = [](const uint2 &q, int z) -> int {
+    return (int)(int16_t)(((z < 2 ? q.x : q.y) >> (16 * (z & 1))) & 0xFFFFu);
+  };
+  const int dump = cap + 2 * lane;
+#pragma unroll 1
+  for (int s0 = 0; s0 < n && fits; s0 += RPS) {
+    const int row = s0 + qr;
+    const bool lr = row < n;
+    int chd = 0, mt = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // child id / own type of `row` from its owner lane
+      const int c2 = __shfl(child[k], (row >> 2) & 63, WAVE);
+      const int t2 = __shfl(myt[k], (row >> 2) & 63, WAVE);
+      if ((row & 3) == k) { chd = c2; mt = t2; }
+    }
+    const int16_t *src = a.wish + (size_t)chd * nw;
+    const int cb = qj * ncq;
+    uint2 q[MAXQ];
+#pragma unroll
+    for (int t = 0; t < MAXQ; ++t) q[t] = load_chunk(src, cb + t);
+    // count: the type's column count per wish (one batch of LDS reads)
+    uint32_t hv[MAXQ][4];
+    int cnt = 0;
+    uint32_t ownc = 0;
+#pragma unroll
+    for (int t = 0; t < MAXQ; ++t) {
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int g = gift_of(q[t], z);
+        const bool ok = lr && (t < ncq) && (cb + t < nch) && (g >= 0);
+        const uint32_t h = thead[ok ? g : 0];
+        hv[t][z] = ok ? h : 0u;
+        cnt += (int)(hv[t][z] >> 8);
+        ownc = (ok && g == mt) ? (uint32_t)(4 * (cb + t) + z + 1) : ownc;
       }
     }
-#pragma unroll
-    for (int u = 0; u < SP_UMAX; ++u) {
-      const int c = lane + WAVE * u;
-      slot[u] = 0;
-      if (c < gch) {
-        const int row = r0 + c / cpr, cc = c - (c / cpr) * cpr;
-        int cnt = 0;
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-          if (z < wpc) {
-            const int g = (int)(int16_t)(((z < 2 ? q[u].x : q[u].y) >> (16 * (z & 1))) & 0xFFFFu);
-            for (int jj = head_get(head32, g); jj >= 0; jj = nxt[jj]) {
-              ++cnt;
-              if (jj == row) own[row] = (uint8_t)(cc * wpc + z + 1);
-            }
-          }
-        }
-        slot[u] = cnt ? (int)(atomicAdd(&gcnt[row - r0], (uint32_t)cnt) | ((uint32_t)cnt << 16)) : 0;
-      }
-    }
-    __syncthreads();
-    const uint32_t v = (lane < grows) ? gcnt[lane] : 0u;
-    const uint32_t incl = wave_incl_scan_u32(v);
+    const uint32_t incl = wave_incl_scan_u32((uint32_t)cnt);
     const int total = __builtin_amdgcn_readlane((int)incl, 63);
-    if (base + total > cap) {  // does not fit: leave the block to the fallback kernel
-      if (lane == 0) {
-        const int p = atomicAdd(a.ovf_cnt, 1);
-        a.ovf_list[p] = b;
-      }
-      return;
+    if (base + total > cap) {
+      fits = false;
+      break;
     }
-    if (lane < grows) off[r0 + lane] = (uint16_t)(base + (int)(incl - v));
-    gcnt[lane] = 0;
-    __syncthreads();
+    const int start = base + (int)incl - cnt;
+    if (lr && qj == 0) off[row] = (uint16_t)start;  // first lane of the row
+    if (ownc) own[row] = (uint8_t)ownc;
+    // fill, half a quarter at a time: first read the (up to 3) columns of
+    // every wish's type in one batch, then write; surplus writes go to the
+    // lane's dump slot, types with >= 4 columns in the block are finished
+    // by the slow loop below
+    int p = start;
+    bool many = false;
 #pragma unroll
-    for (int u = 0; u < SP_UMAX; ++u) {
-      const int c = lane + WAVE * u;
-      if (c < gch && slot[u]) {
-        const int row = r0 + c / cpr, cc = c - (c / cpr) * cpr;
-        int p = (int)off[row] + (slot[u] & 0xFFFF);
+    for (int h2 = 0; h2 < 2; ++h2) {
+      uint32_t c3[MAXQ / 2][4];
+#pragma unroll
+      for (int t = h2 * (MAXQ / 2); t < (h2 + 1) * (MAXQ / 2); ++t)
 #pragma unroll
         for (int z = 0; z < 4; ++z) {
-          if (z < wpc) {
-            const int g = (int)(int16_t)(((z < 2 ? q[u].x : q[u].y) >> (16 * (z & 1))) & 0xFFFFu);
-            // the tile byte is code - (n_wish + 1), a negative int8 (0 = miss)
-            const uint32_t tb = ((uint32_t)(cc * wpc + z - nw) & 0xFFu) << 8;
-            for (int jj = head_get(head32, g); jj >= 0; jj = nxt[jj]) hits[p++] = (uint16_t)(tb | (uint32_t)jj);
-          }
+          const int e = (int)(hv[t][z] & 0xFFu);  // first column of the type in csort
+          c3[t - h2 * (MAXQ / 2)][z] = (uint32_t)csort[e] | ((uint32_t)csort[e + 1] << 8) |
+                                       ((uint32_t)csort[e + 2] << 16);
         }
-      }
+#pragma unroll
+      for (int t = h2 * (MAXQ / 2); t < (h2 + 1) * (MAXQ / 2); ++t)
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          const int cg = (int)(hv[t][z] >> 8);
+          const uint32_t cc = c3[t - h2 * (MAXQ / 2)][z];
+          const uint32_t tb = ((uint32_t)(4 * (cb + t) + z - nw) & 0xFFu) << 8;
+          hits[cg >= 1 ? p : dump] = (uint16_t)(tb | (cc & 0xFFu));
+          hits[cg >= 2 ? p + 1 : dump] = (uint16_t)(tb | ((cc >> 8) & 0xFFu));
+          hits[cg >= 3 ? p + 2 : dump] = (uint16_t)(tb | (cc >> 16));
+          many |= cg >= 4;
+          p += cg;
+        }
+    }
+    if (__builtin_expect(__any(many), 0)) {  // types with 4+ columns in this block
+      int pp = start;
+#pragma unroll
+      for (int t = 0; t < MAXQ; ++t)
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          const int cg = (int)(hv[t][z] >> 8);
+          const int e = (int)(hv[t][z] & 0xFFu);
+          const uint32_t tb = ((uint32_t)(4 * (cb + t) + z - nw) & 0xFFu) << 8;
+          for (int x = 3; x < cg; ++x) hits[pp + x] = (uint16_t)(tb | csort[e + x]);
+          pp += cg;
+        }
     }
     base += total;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int x = 0; x < 3; ++x) asm volatile("" ::"v"(warm[k][x]));
+  if (!fits) {  // does not fit: leave the block to the fallback kernel
+    if (lane == 0) {
+      const int p = atomicAdd(a.ovf_cnt, 1);
+      a.ovf_list[p] = b;
+    }
+    return;
   }
   if (lane == 0) off[n] = (uint16_t)base;
   __syncthreads();
@@ -1791,6 +1868,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     const int r = 4 * lane + k;
     offr[k] = (r < n) ? (int)((uint32_t)off[r] | ((uint32_t)off[r + 1] << 16)) : 0;
   }
+  const uint64_t t1 = (a.flags & SH_FLAG_TIMING) ? wall_clock64() : 0;
   __syncthreads();  // the build area becomes the solve area (u, rem, vrow)
   for (int r = lane; r < n; r += WAVE) u_l[r] = 0;
 
@@ -1955,6 +2033,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   }
   __syncthreads();
 
+  const uint64_t t2 = (a.flags & SH_FLAG_TIMING) ? wall_clock64() : 0;
   // -- outputs: lane handles rows i = 4*lane + k ------------------------------------
   int64_t cost = 0, dch = 0, dgh = 0;
 #pragma unroll
@@ -1989,6 +2068,12 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   if (lane == 0) {
     if (a.cost) a.cost[b] = cost;
     if (a.steps) a.steps[b] = steps;
+    if (a.flags & SH_FLAG_TIMING) {
+      const uint64_t t3 = wall_clock64();
+      if (a.col) a.col[(size_t)b * n] = (int32_t)(tc - t0);  // column sort done
+      auto c21 = [](uint64_t x) { return x < 0x1FFFFFull ? x : 0x1FFFFFull; };
+      a.steps[b] = (int64_t)(c21(t1 - t0) | (c21(t2 - t0) << 21) | (c21(t3 - t0) << 42));
+    }
     if (a.delta) {
       atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
       atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
@@ -2269,11 +2354,15 @@ struct sh_ctx {
 namespace {
 constexpr int SP_DEFAULT_BUDGET = 160 * 1024 / 8;  // 8 blocks (waves) per CU
 
+// Hit-list capacity (entries) of the sparse kernel under the LDS budget: what
+// is left after the fixed state and the 64 dump dwords; the hit area also has
+// to hold the counting-sort scratch (ng x u32), which may exceed the budget.
 int sp_capacity(const sh_ctx *ctx) {
   const SpLds L0 = sp_lds_layout(ctx->ng, 0);
   const size_t budget = (size_t)(ctx->sp_budget > 0 ? ctx->sp_budget : SP_DEFAULT_BUDGET);
-  if (budget <= L0.total) return 0;
-  const size_t cap = (budget - L0.total) / 2;
+  const size_t fixed = L0.hits + 2 * 64 * 2;
+  if (budget <= fixed) return 0;
+  const size_t cap = (budget - fixed) / 2;
   return (int)std::min<size_t>(cap & ~(size_t)7, 65528);
 }
 }  // namespace
@@ -2466,7 +2555,10 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   a.ovf_cnt = ctx->d_ovf + p;
   a.ovf_list = ctx->d_ovf + 2 + (size_t)p * ctx->ovf_cap;
   a.blist = nullptr;
-  hipLaunchKernelGGL(santa_sp_kernel, dim3(B), dim3(WAVE), L.total, s, a);
+  if (ctx->n_wish % 4 == 0)
+    hipLaunchKernelGGL(santa_sp_kernel<true>, dim3(B), dim3(WAVE), L.total, s, a);
+  else
+    hipLaunchKernelGGL(santa_sp_kernel<false>, dim3(B), dim3(WAVE), L.total, s, a);
   HIP_TRY(hipGetLastError());
   SantaArgs f = a;
   f.blist = a.ovf_list;

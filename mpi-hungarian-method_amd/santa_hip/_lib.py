@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsanta_hip.so")
+LIB_PATH = os.environ.get("SANTA_HIP_LIB") or os.path.join(_HERE, "libsanta_hip.so")
 
 SH_OK = 0
 SH_ERR_INFEASIBLE = -1
@@ -24,6 +24,7 @@ SH_FLAG_BUILD_ONLY = 4
 SH_FLAG_LDS_TILE = 8
 SH_FLAG_SW_TILE = 16
 SH_FLAG_VT_TILE = 32
+SH_FLAG_TIMING = 64
 SH_MAX_N = 1024
 SH_MAX_N_SANTA = 256
 

@@ -7,7 +7,7 @@ subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx9
                stderr=subprocess.DEVNULL)
 s = open("/tmp/sh.s").read()
 name = sys.argv[1]
-a = s.index(name + "ENS_9SantaArgsE:") if "santa" in name else s.index(name)
+a = s.index(name)
 b = s.index(".Lfunc_end", a)
 body = s[a:b].splitlines()
 idx = [i for i, l in enumerate(body) if "v_min_u32_dpp" in l][0]

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--phase", choices=["all", "build", "solve", "score"], default="all")
     ap.add_argument("--flags", type=int, default=0, help="extra SH_FLAG_* bits (8 = LDS tile)")
     ap.add_argument("--budget", type=int, default=0, help="sparse kernel LDS bytes per block (0 = default)")
+    ap.add_argument("--timing", action="store_true", help="per-phase in-kernel timing (sparse kernel)")
     ap.add_argument("--state-round", type=int, default=0,
                     help="time round R of the optimisation: first apply rounds 0..R-1 (default kernel)")
     a = ap.parse_args()
@@ -61,6 +62,19 @@ def main():
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
         out["score"] = {"ms": min(ts), "all_ms": ts}
+    if a.timing:  # dev: per-phase wall-clock ticks of the sparse kernel (100 MHz)
+        t = base.clone()
+        col = torch.zeros(B * a.n, dtype=torch.int32, device="cuda")
+        ctx.solve_blocks(a.mode, rows, a.n, t, steps=steps, col=col, flags=_lib.SH_FLAG_TIMING | a.flags)
+        out["colsort_us"] = float(col.view(B, a.n)[:, 0].cpu().numpy().astype(float).mean()) / 100.0
+        v = steps.cpu().numpy().astype("uint64")
+        ph = [(v & 0x1FFFFF), (v >> 21) & 0x1FFFFF, (v >> 42) & 0x1FFFFF]
+        built, solved, done = [x.astype(float) / 100.0 for x in ph]  # us
+        out["timing_us"] = {"build_mean": built.mean(), "build_max": built.max(),
+                            "solve_mean": (solved - built).mean(), "solve_max": (solved - built).max(),
+                            "epilogue_mean": (done - solved).mean(), "total_max": done.max()}
+        steps.zero_()
+        ctx.solve_blocks(a.mode, rows, a.n, base.clone(), steps=steps, flags=a.flags)
     out["blocks"] = B
     out["budget"] = a.budget
     out["cap"] = cap
