@@ -58,6 +58,10 @@ extern "C" {
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024
+/* Largest Santa block of sh_solve_blocks (rows; pairs in twins mode): the
+ * reference's own sizes are 2000 singles and 3000 pairs.  n <= 256 runs the
+ * on-chip tile kernels, larger blocks rebuild each row from the wishlist. */
+#define SH_MAX_N_SANTA 4096
 
 typedef struct sh_ctx sh_ctx;
 
@@ -111,7 +115,7 @@ int sh_sample_blocks(uint64_t seed, uint64_t round, int lo, int count, int strid
  *   d_delta int64 [2]     (nullable)  += (dS_child, dS_gift) of the applied
  *                                        swaps (integer, order-free)
  *   d_steps int64 [B]     (nullable)  Dijkstra steps taken per block
- * Returns SH_ERR_ARGS for n > SH_MAX_N or rows out of range (checked on the
+ * Returns SH_ERR_ARGS for n > SH_MAX_N_SANTA or rows out of range (checked on the
  * device lazily: an out-of-range block is skipped and reported by
  * sh_ctx_error_flags).
  * ------------------------------------------------------------------------ */

@@ -373,9 +373,14 @@ __device__ __forceinline__ uint64_t block_min_u64(uint64_t wmin, uint64_t *slots
   }
 }
 
-template <int NW, int K, typename Loader>
+template <int NW, int K, typename Loader, int FB = 10>
 __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, int64_t &steps_out,
                              int &fallbacks, const bool exact) {
+  // key fields: FB bits of position and of row/column (n <= 2^FB), 1 class bit
+  constexpr int LOB = 2 * FB + 1;
+  constexpr uint32_t FM = (1u << FB) - 1u;
+  constexpr uint64_t HI_MAX = (1ull << (64 - LOB)) - 1;
+  constexpr int64_t BIAS = 1ll << (63 - LOB);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t INF = INT64_MAX;
   int64_t spc[K], nv[K];  // nv = -v (column duals, negated)
@@ -385,6 +390,10 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
     nv[k] = 0;
     path[k] = -1;
   }
+  auto lo_of = [&](int k, int j) -> uint32_t {
+    return (r4c[k] < 0) ? (((FM - (uint32_t)pos[k]) << FB) | (uint32_t)j)
+                        : ((1u << (2 * FB)) | ((uint32_t)pos[k] << FB) | (uint32_t)r4c[k]);
+  };
   int64_t steps = 0;
   int par = 0;
   for (int cur = 0; cur < n; ++cur) {
@@ -405,7 +414,7 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
       int64_t c[K];
       ld.load(i, c);
       const int64_t kU = minVal - ui;
-      const uint64_t kb = (uint64_t)KEY_BIAS - (uint64_t)minVal;
+      const uint64_t kb = (uint64_t)BIAS - (uint64_t)minVal;
       uint64_t best = ~0ull;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -415,18 +424,17 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
         const bool upd = act && (r < spc[k]);
         spc[k] = upd ? r : spc[k];
         path[k] = upd ? i : path[k];
-        const uint32_t lo = (r4c[k] < 0)
-                                ? (((uint32_t)(1023 - pos[k]) << 10) | (uint32_t)j)
-                                : ((1u << 20) | ((uint32_t)pos[k] << 10) | (uint32_t)r4c[k]);
-        const uint64_t key = (key_hi_of((uint64_t)spc[k] + kb) << KEY_LO_BITS) | lo;
+        const uint64_t sb = (uint64_t)spc[k] + kb;
+        const uint64_t kh = (sb <= HI_MAX) ? sb : (((int64_t)sb < 0) ? 0 : HI_MAX);
+        const uint64_t key = (kh << LOB) | lo_of(k, j);
         best = umin64(best, act ? key : ~0ull);
       }
       uint64_t g = block_min_u64<NW>(wave_min_u64_fast(best), S.red + par * NW, w);
       g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
       par ^= 1;
-      const uint64_t hi = g >> KEY_LO_BITS;
-      if (exact || hi == 0 || hi == KEY_HI_MAX) {
+      const uint64_t hi = g >> LOB;
+      if (exact || hi == 0 || hi == HI_MAX) {
         // exact two-pass argmin: min spc (signed), then min key-low among ties
         uint64_t m = ~0ull;
 #pragma unroll
@@ -438,23 +446,18 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const int j = w * (WAVE * K) + k * WAVE + lane;
-          if (pos[k] >= 0 && spc[k] == ms) {
-            const uint32_t lo = (r4c[k] < 0)
-                                    ? (((uint32_t)(1023 - pos[k]) << 10) | (uint32_t)j)
-                                    : ((1u << 20) | ((uint32_t)pos[k] << 10) | (uint32_t)r4c[k]);
-            b2 = umin64(b2, lo);
-          }
+          if (pos[k] >= 0 && spc[k] == ms) b2 = umin64(b2, lo_of(k, j));
         }
         g = block_min_u64<NW>(wave_min_u64_dpp(b2), S.red + 3 * NW, w);
         minVal = ms;
         ++fallbacks;
       } else {
-        minVal = minVal + ((int64_t)hi - KEY_BIAS);
+        minVal = minVal + ((int64_t)hi - BIAS);
       }
-      const bool assigned = (g >> 20) & 1u;
-      const int pk = (int)((g >> 10) & 1023u);
-      const int aux = (int)(g & 1023u);
-      const int pstar = assigned ? pk : 1023 - pk;
+      const bool assigned = (g >> (2 * FB)) & 1u;
+      const int pk = (int)((g >> FB) & FM);
+      const int aux = (int)(g & FM);
+      const int pstar = assigned ? pk : (int)FM - pk;
       const int last = nrem - 1;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -2083,6 +2086,235 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Large-block Santa kernel (256 < n <= 4096, both modes): the reference's own
+// block sizes (2000 singles, mpi_single.py:238; 3000 pairs, mpi_twins.py:244).
+//
+// The n x n tile does not fit on chip (4 MB at n = 2000), so a Dijkstra step
+// rebuilds row i on the fly: the child's wishlist row (200 B from HBM/L2,
+// read by 25 threads; twins: both children) is looked up in an LDS table of
+// the block's columns sorted by gift type (type -> start, count), and each
+// wish's rank code is scattered into an n-byte LDS row buffer; after one
+// barrier every thread reads (and clears) the codes of its K columns.  The
+// solve is sap_solve_mw (scipy's SAP, NW waves, packed-key DPP argmin, 12-bit
+// key fields above n = 1024).  Outputs: the matched codes are recovered by
+// scanning the child's wishlist for the new and old gift (exact cost and
+// happiness deltas), then the in-place apply.
+// ---------------------------------------------------------------------------
+template <int MODE, int NW, int K>
+struct WishRowLoader {
+  const int16_t *wish;
+  const int32_t *rows;    // LDS [n]
+  const uint32_t *thead;  // LDS [ng]: end in csort | count << 16
+  const uint16_t *csort;  // LDS [n]
+  uint8_t *rowbuf;        // LDS [n] (singles) / [2n] (twins: c1 | c2 << 8)
+  int n, nw, nw1;
+  int64_t E;
+  __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int nch = (nw + 3) >> 2;
+    if (tid < (MODE ? 2 : 1) * nch) {
+      const int vr = MODE ? (tid >= nch) : 0;
+      const int cc = tid - vr * nch;
+      const int16_t *src = wish + (size_t)(rows[i] + vr) * nw;
+      uint32_t g4[4];
+      if ((nw & 3) == 0) {
+        const uint2 q = *(const uint2 *)(src + 4 * cc);
+        g4[0] = q.x & 0xFFFFu; g4[1] = q.x >> 16; g4[2] = q.y & 0xFFFFu; g4[3] = q.y >> 16;
+      } else {
+#pragma unroll
+        for (int z = 0; z < 4; ++z) g4[z] = (4 * cc + z < nw) ? (uint16_t)src[4 * cc + z] : 0xFFFFu;
+      }
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int g = (int)(int16_t)g4[z];
+        if (g >= 0) {
+          const uint32_t h = thead[g];
+          const int cnt = (int)(h >> 16), e = (int)(h & 0xFFFFu);
+          const uint8_t code = (uint8_t)(4 * cc + z + 1);
+          for (int x = e - cnt; x < e; ++x) rowbuf[MODE ? 2 * csort[x] + vr : csort[x]] = code;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int j = w * (WAVE * K) + k * WAVE + lane;
+      if (j < n) {
+        if (MODE) {
+          uint16_t *rb = (uint16_t *)rowbuf;
+          c[k] = twin_cost(rb[j], nw1, E);
+          rb[j] = 0;
+        } else {
+          c[k] = single_cost(rowbuf[j], nw1, E);
+          rowbuf[j] = 0;
+        }
+      } else {
+        c[k] = 0;
+      }
+    }
+  }
+};
+
+struct BigLds {
+  size_t u, c4r, r4c, path, red, rows, ctype, csort, thead, rowbuf, part, scan, total;
+};
+
+__host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int ng, int nw) {
+  BigLds L;
+  size_t o = 0;
+  L.u = o;      o += r16((size_t)n * 8);
+  L.c4r = o;    o += r16((size_t)n * 2);
+  L.r4c = o;    o += r16((size_t)n * 2);
+  L.path = o;   o += r16((size_t)n * 2);
+  L.red = o;    o += r16((size_t)4 * nw * 8);
+  L.rows = o;   o += r16((size_t)n * 4);
+  L.ctype = o;  o += r16((size_t)n * 2);
+  L.csort = o;  o += r16((size_t)n * 2);
+  L.thead = o;  o += r16((size_t)ng * 4);
+  L.rowbuf = o; o += r16((size_t)n * (mode ? 2 : 1));
+  L.part = o;   o += r16((size_t)nw * 3 * 8);
+  L.scan = o;   o += r16((size_t)nw * 4);
+  L.total = o;
+  return L;
+}
+
+// code of gift type t in child's wishlist (rank + 1), 0 = not wished
+__device__ __forceinline__ uint32_t wish_code(const SantaArgs &a, int child, int t) {
+  const int16_t *src = a.wish + (size_t)child * a.n_wish;
+  for (int r = 0; r < a.n_wish; ++r)
+    if (src[r] == t) return (uint32_t)(r + 1);
+  return 0u;
+}
+
+template <int MODE, int NW, int K, int FB>
+__global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int WG = NW * WAVE;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = a.n;
+  const BigLds L = big_lds_layout(n, MODE, a.ng, NW);
+  SolveLds S{(int64_t *)(smem + L.u), (int16_t *)(smem + L.c4r), (int16_t *)(smem + L.r4c),
+             (int16_t *)(smem + L.path), (uint64_t *)(smem + L.red)};
+  int32_t *rows_l = (int32_t *)(smem + L.rows);
+  int16_t *ctype = (int16_t *)(smem + L.ctype);
+  uint16_t *csort = (uint16_t *)(smem + L.csort);
+  uint32_t *thead = (uint32_t *)(smem + L.thead);
+  uint8_t *rowbuf = smem + L.rowbuf;
+  int64_t *part = (int64_t *)(smem + L.part);
+  uint32_t *scan = (uint32_t *)(smem + L.scan);
+
+  // -- rows, range check ---------------------------------------------------------
+  int bad = 0;
+  for (int j = tid; j < n; j += WG) {
+    const int r = a.rows[(size_t)b * n + j];
+    bad |= (r < 0) || (r + MODE >= a.nc);
+    rows_l[j] = r;
+  }
+  if (__syncthreads_or(bad)) {
+    if (tid == 0) atomicOr(a.err, 1);
+    return;
+  }
+  for (int t = tid; t < a.ng; t += WG) thead[t] = 0u;
+  for (int q = tid; q < n * (MODE ? 2 : 1); q += WG) rowbuf[q] = 0;
+  for (int i = tid; i < n; i += WG) {
+    S.u[i] = 0;
+    S.c4r[i] = -1;
+    S.r4c[i] = -1;
+  }
+  __syncthreads();
+  // -- columns sorted by gift type (counting sort) ----------------------------------
+  for (int j = tid; j < n; j += WG) {
+    const int ty = a.types[rows_l[j]];
+    ctype[j] = (int16_t)ty;
+    atomicAdd(&thead[ty], 1u << 16);
+  }
+  __syncthreads();
+  {  // block-wide exclusive scan of the counts over types
+    const int per = (a.ng + WG - 1) / WG;
+    const int t0 = tid * per, t1 = min(a.ng, t0 + per);
+    uint32_t sum = 0;
+    for (int t = t0; t < t1; ++t) sum += thead[t] >> 16;
+    const uint32_t incl = wave_incl_scan_u32(sum);
+    if (lane == 63) scan[w] = incl;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (int q = 0; q < w; ++q) wbase += scan[q];
+    uint32_t run = wbase + incl - sum;
+    for (int t = t0; t < t1; ++t) {
+      const uint32_t h = thead[t];
+      thead[t] = h | run;  // low half: fill cursor from the type's start
+      run += h >> 16;
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < n; j += WG) csort[atomicAdd(&thead[ctype[j]], 1u) & 0xFFFFu] = (uint16_t)j;
+  __syncthreads();  // thead = end of the type's run | count << 16
+
+  // -- solve ------------------------------------------------------------------------
+  int64_t steps = 0;
+  int fallbacks = 0;
+  const int nw1 = a.n_wish + 1;
+  if (a.flags & SH_FLAG_BUILD_ONLY) {
+    for (int i = tid; i < n; i += WG) S.c4r[i] = (int16_t)i;
+    __syncthreads();
+  } else {
+    const WishRowLoader<MODE, NW, K> ld{a.wish, rows_l, thead, csort, rowbuf, n, a.n_wish, nw1, a.E};
+    sap_solve_mw<NW, K, WishRowLoader<MODE, NW, K>, FB>(n, ld, S, steps, fallbacks,
+                                                         (a.flags & SH_FLAG_EXACT_ARGMIN) != 0);
+  }
+  // -- outputs ----------------------------------------------------------------------
+  int64_t cost = 0, dch = 0, dgh = 0;
+  for (int i = tid; i < n; i += WG) {
+    const int col = S.c4r[i];
+    const int told = ctype[i], tnew = ctype[col];
+    const int child = rows_l[i];
+    const uint32_t n1 = wish_code(a, child, tnew), o1 = wish_code(a, child, told);
+    if (MODE == 0) {
+      cost += single_cost(n1, nw1, a.E);
+      dch += child_happy(n1, nw1) - child_happy(o1, nw1);
+      dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
+    } else {
+      const uint32_t n2 = wish_code(a, child + 1, tnew), o2 = wish_code(a, child + 1, told);
+      cost += twin_cost(n1 | (n2 << 8), nw1, a.E);
+      dch += child_happy(n1, nw1) + child_happy(n2, nw1) - child_happy(o1, nw1) - child_happy(o2, nw1);
+      dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
+             gift_happy(a, child, told) - gift_happy(a, child + 1, told);
+    }
+    if (a.col) a.col[(size_t)b * n + i] = col;
+  }
+  cost = wave_sum_i64(cost);
+  dch = wave_sum_i64(dch);
+  dgh = wave_sum_i64(dgh);
+  if (lane == 0) {
+    part[3 * w + 0] = cost;
+    part[3 * w + 1] = dch;
+    part[3 * w + 2] = dgh;
+  }
+  __syncthreads();  // every old type was read from ctype (LDS): apply in place
+  for (int i = tid; i < n; i += WG) {
+    const int16_t tnew = ctype[S.c4r[i]];
+    a.types[rows_l[i]] = tnew;
+    if (MODE) a.types[rows_l[i] + 1] = tnew;
+  }
+  if (tid == 0) {
+    int64_t tc = 0, t0 = 0, t1 = 0;
+    for (int q = 0; q < NW; ++q) {
+      tc += part[3 * q];
+      t0 += part[3 * q + 1];
+      t1 += part[3 * q + 2];
+    }
+    if (a.cost) a.cost[b] = tc;
+    if (a.steps) a.steps[b] = steps;
+    if (a.delta) {
+      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)t0);
+      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)t1);
+    }
+    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Generic batched LSAP.  int64 paths use the multi-wave solver (rows streamed
 // from global memory, or generated by hash); float64 uses the single-wave
 // scipy-replay solver sap_solve<K, double>.
@@ -2533,6 +2765,31 @@ int launch_santa_vt(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s)
   return SH_OK;
 }
 
+template <int MODE, int NW, int K, int FB>
+int launch_big_cfg(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
+  const BigLds L = big_lds_layout(a.n, MODE, ctx->ng, NW);
+  if (L.total > 160 * 1024) return fail(SH_ERR_ARGS, "block too large for LDS");
+  static thread_local size_t attr_set = 0;
+  if (L.total > 64 * 1024 && L.total > attr_set) {
+    HIP_TRY(hipFuncSetAttribute((const void *)santa_big_kernel<MODE, NW, K, FB>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total));
+    attr_set = L.total;
+  }
+  hipLaunchKernelGGL((santa_big_kernel<MODE, NW, K, FB>), dim3(B), dim3(NW * WAVE), L.total, s, a);
+  HIP_TRY(hipGetLastError());
+  return SH_OK;
+}
+
+template <int MODE>
+int launch_santa_big(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
+  const int n = a.n;
+  if (n <= 512) return launch_big_cfg<MODE, 8, 1, 10>(ctx, a, B, s);
+  if (n <= 1024) return launch_big_cfg<MODE, 16, 1, 10>(ctx, a, B, s);
+  if (n <= 2048) return launch_big_cfg<MODE, 16, 2, 12>(ctx, a, B, s);
+  if (n <= 3072) return launch_big_cfg<MODE, 16, 3, 12>(ctx, a, B, s);
+  return launch_big_cfg<MODE, 16, 4, 12>(ctx, a, B, s);
+}
+
 // Sparse-tile kernel + the fallback launch for blocks whose hit lists did not
 // fit.  The two overflow counters alternate between calls: the fallback
 // launch of call k resets the counter that call k+1 appends to.
@@ -2578,7 +2835,8 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
                     unsigned flags, void *stream) {
   if (!ctx || !d_rows || !d_types) return fail(SH_ERR_ARGS, "null pointer");
   if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS) return fail(SH_ERR_ARGS, "bad mode");
-  if (n <= 0 || n > 256) return fail(SH_ERR_ARGS, "n must be in [1, 256] for the LDS-tile path");
+  if (n <= 0 || n > SH_MAX_N_SANTA) return fail(SH_ERR_ARGS, "n must be in [1, 4096]");
+  if ((int64_t)n * (mode ? 2 : 1) > ctx->nc) return fail(SH_ERR_ARGS, "block larger than the instance");
   if (B < 0) return fail(SH_ERR_ARGS, "B < 0");
   if (B == 0) return SH_OK;
   SantaArgs a;
@@ -2589,6 +2847,8 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   a.cap = 0; a.ovf_cnt = nullptr; a.ovf_list = nullptr;
   a.blist = nullptr; a.bcount = nullptr; a.ovf_reset = nullptr;
   hipStream_t s = (hipStream_t)stream;
+  if (n > 256)
+    return mode == SH_MODE_SINGLE ? launch_santa_big<0>(ctx, a, B, s) : launch_santa_big<1>(ctx, a, B, s);
   if (flags & SH_FLAG_LDS_TILE)
     return mode == SH_MODE_SINGLE ? launch_santa<1, 0>(ctx, a, B, s) : launch_santa<1, 1>(ctx, a, B, s);
   // twins keep the LDS tile: their 128-dword register column does not stay

@@ -26,7 +26,7 @@ SH_FLAG_SW_TILE = 16
 SH_FLAG_VT_TILE = 32
 SH_FLAG_TIMING = 64
 SH_MAX_N = 1024
-SH_MAX_N_SANTA = 256
+SH_MAX_N_SANTA = 4096
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

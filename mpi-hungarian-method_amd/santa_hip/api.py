@@ -79,7 +79,7 @@ def _solve_one(mode: int, rows: np.ndarray, types_np: np.ndarray) -> np.ndarray:
     s = session()
     n = rows.shape[0]
     if n > _lib.SH_MAX_N_SANTA:
-        raise ValueError(f"block of {n} rows > {_lib.SH_MAX_N_SANTA} (LDS-tile path)")
+        raise ValueError(f"block of {n} rows > {_lib.SH_MAX_N_SANTA}")
     rows_t = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int32)).to(s.device)
     types = s.upload_types(types_np)
     col = torch.empty(n, dtype=torch.int32, device=s.device)

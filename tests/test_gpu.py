@@ -112,7 +112,12 @@ def test_santa_blocks_golden(sh, ctx, full_data, santa_blocks):
 
 
 @pytest.mark.parametrize("mode,n,B", [(0, 256, 64), (0, 64, 40), (0, 100, 16), (1, 256, 8),
-                                      (1, 37, 9)])
+                                      (1, 37, 9),
+                                      # large blocks (row rebuilt from the wishlist per step),
+                                      # up to the reference's own sizes (mpi_single.py:238,
+                                      # mpi_twins.py:244)
+                                      (0, 257, 3), (0, 700, 2), (0, 1024, 2), (0, 2000, 2),
+                                      (1, 300, 2), (1, 1500, 1), (1, 3000, 1)])
 def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
     """Fused build+solve+apply on the GPU equals the CPU oracle: col, exact
     cost, the whole new type vector, and the happiness deltas."""
@@ -170,6 +175,37 @@ def test_full_round_properties(sh, ctx, full_data):
     assert np.array_equal(c[pick], ocol)
     assert np.array_equal(cost.cpu().numpy()[pick], ocost)
     assert np.array_equal(t1[r[pick].reshape(-1)], t_host[r[pick].reshape(-1)])
+
+
+@pytest.mark.parametrize("mode,n", [(0, 2000), (1, 3000)])
+def test_full_round_reference_block_sizes(sh, ctx, full_data, mode, n):
+    """A full round at the reference's default block sizes (477 blocks of 2000
+    singles, mpi_single.py:238-240; 6 blocks of 3000 pairs,
+    mpi_twins.py:244-246): invariants, delta = rescore, and blocks spot-checked
+    against the oracle."""
+    _, _, _, nb = ctx.geometry(mode, n)
+    assert nb == (477 if mode == 0 else 6)
+    rows = ctx.sample_blocks(mode, n, nb, 4, 0)
+    types = ctx.upload_types(full_data.types)
+    cost = torch.empty(nb, dtype=torch.int64, device="cuda")
+    col = torch.empty(nb * n, dtype=torch.int32, device="cuda")
+    delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+    s0 = ctx.score_sums(types)
+    ctx.solve_blocks(mode, rows, n, types, col=col, cost=cost, delta=delta)
+    s1 = ctx.score_sums(types)
+    assert ctx.error_flags() == 0
+    t1 = types.cpu().numpy()
+    assert np.array_equal(np.bincount(t1, minlength=1000), np.bincount(full_data.types, minlength=1000))
+    c = col.cpu().numpy().reshape(nb, n)
+    assert (np.sort(c, axis=1) == np.arange(n)).all()
+    assert delta.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]]
+    assert s1[2] == 0 and s1[3] == 0
+    r = rows.cpu().numpy().reshape(nb, n)
+    pick = np.random.default_rng(1).choice(nb, 2, replace=False)
+    t_host = full_data.types.copy()
+    ocol, ocost = oracle.round_blocks(mode, full_data.wish, t_host, r[pick], ng=full_data.ng)
+    assert np.array_equal(c[pick], ocol)
+    assert np.array_equal(cost.cpu().numpy()[pick], ocost)
 
 
 # --------------------------------------------------------------------------- score
@@ -245,7 +281,7 @@ def test_error_paths(sh, ctx, full_data):
     assert ctx.error_flags() & 1
     assert np.array_equal(types.cpu().numpy(), full_data.types)  # skipped block wrote nothing
     with pytest.raises(ValueError):
-        ctx.solve_blocks(0, torch.zeros(512, dtype=torch.int32, device="cuda"), 512, types)
+        ctx.solve_blocks(0, torch.zeros(5000, dtype=torch.int32, device="cuda"), 5000, types)
     with pytest.raises(ValueError):
         ctx.sample_blocks(0, 256, 5000, 1, 0)
     with pytest.raises(ValueError):
