@@ -17,7 +17,7 @@ with np.random.permutation replaced by the build's seeded Feistel
 permutation so that the block sequence is reproducible.  Nothing of the
 reference's source is written to disk; only data (npz/json) is.
 
-Usage: python tests/golden/make_golden.py [--skip-trajectory]
+Usage: python tests/golden/make_golden.py [--only lsap,blocks,large,score,traj]
 """
 from __future__ import annotations
 
@@ -201,6 +201,54 @@ def make_santa_blocks(sd: D.SantaData, out: str) -> None:
     print(f"santa_blocks: {k} blocks -> {out} ({os.path.getsize(out)} B)")
 
 
+def make_santa_blocks_large(sd: D.SantaData, out: str) -> None:
+    """One block at each of the reference's own default sizes: 2000 singles
+    (mpi_single.py:238) and 3000 twin pairs (mpi_twins.py:244, block_size
+    6000 children), solved by the reference's optimize_block(_twins)."""
+    ns1 = extract(os.path.join(REF, "mpi_single.py"), ["optimize_block"])
+    ns2 = extract(os.path.join(REF, "mpi_twins.py"), ["optimize_block_twins"])
+    import pandas as pd
+    nc, ng, nq = sd.nc, sd.ng, sd.nq
+    tri, tw = sd.families
+    table = LazyHappiness(sd.wish, ng)
+    gift_ids = np.array([[g] * nq for g in range(ng)]).flatten()
+    slots = D.slot_ids(sd.types, nq)
+    subm = pd.DataFrame({"ChildId": np.arange(nc), "GiftId": sd.types.astype(np.int64)})
+    arrays, meta = {}, []
+    n = 2000
+    lo, count, _ = S.single_geometry(nc, n, tri, tw)
+    blk = S.sample_blocks(21, 0, lo, count, 1, n, 1)[0].astype(np.int64)
+    ns1.update(block_size=n, gift_ids=gift_ids, child_happiness=table)
+    t = time.time()
+    cids, gids = ns1["optimize_block"](blk, current_gift_ids=slots)
+    gift_block = slots[blk]
+    pos = {int(s_): j for j, s_ in enumerate(gift_block)}
+    col = np.array([pos[int(g)] for g in gids], dtype=np.int16)
+    C = np.array([[table[c][gift_ids[gift_block[j]]] for j in range(n)] for c in blk], dtype=np.float64)
+    arrays["rows0"], arrays["col0"] = blk.astype(np.int32), col
+    meta.append({"i": 0, "mode": "single", "n": n,
+                 "cost_units": int(round(C[np.arange(n), col].sum() * 2 ** 31)),
+                 "seconds": time.time() - t})
+    pairs = 3000
+    lo, count, _ = S.twin_geometry(tri, tw, pairs)
+    blk = S.sample_blocks(23, 0, lo, count, 2, pairs, 1)[0].astype(np.int64)
+    ns2.update(block_size=2 * pairs, child_happiness=table)
+    t = time.time()
+    cids, gids = ns2["optimize_block_twins"](blk, subm)
+    gift_block = subm["GiftId"][blk].values
+    C = np.array([[table[c][g] + table[c + 1][g] for g in gift_block] for c in blk], dtype=np.float64)
+    from scipy.optimize import linear_sum_assignment as lsa
+    _, col = lsa(C)
+    assert np.array_equal(gift_block[col], gids)
+    arrays["rows1"], arrays["col1"] = blk.astype(np.int32), col.astype(np.int16)
+    meta.append({"i": 1, "mode": "twins", "n": pairs,
+                 "cost_units": int(round(C[np.arange(pairs), col].sum() * 2 ** 31)),
+                 "seconds": time.time() - t})
+    arrays["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(out, **arrays)
+    print(f"santa_blocks_large: {meta} -> {out} ({os.path.getsize(out)} B)")
+
+
 # ---------------------------------------------------------------------------
 def reference_score(ns, sd: D.SantaData, types: np.ndarray) -> float:
     pred = np.stack([np.arange(sd.nc), types.astype(np.int64)], axis=1)
@@ -372,12 +420,14 @@ def main():
     todo = args.only.split(",")
     if "all" in todo or "lsap" in todo:
         make_lsap_cases(os.path.join(HERE, "lsap_cases.npz"))
-    if set(todo) & {"all", "blocks", "score", "traj"}:
+    if set(todo) & {"all", "blocks", "large", "score", "traj"}:
         t = time.time()
         sd = D.synthetic(2017)
         print(f"synthetic data {time.time() - t:.1f}s")
         if "all" in todo or "blocks" in todo:
             make_santa_blocks(sd, os.path.join(HERE, "santa_blocks.npz"))
+        if "all" in todo or "large" in todo:
+            make_santa_blocks_large(sd, os.path.join(HERE, "santa_blocks_large.npz"))
         if "all" in todo or "score" in todo:
             make_score(sd, os.path.join(HERE, "santa_score.json"))
         if "all" in todo or "traj" in todo:

@@ -111,6 +111,23 @@ def test_santa_blocks_golden(sh, ctx, full_data, santa_blocks):
     assert ctx.error_flags() == 0
 
 
+def test_santa_blocks_golden_reference_sizes(sh, ctx, full_data):
+    """The reference's optimize_block at its default 2000 and
+    optimize_block_twins at 3000 pairs (golden, made from the reference)."""
+    from conftest import load_npz_cases
+    z, meta = load_npz_cases("santa_blocks_large.npz")
+    for m in meta:
+        k, n = m["i"], m["n"]
+        types = ctx.upload_types(full_data.types)
+        col = torch.empty(n, dtype=torch.int32, device="cuda")
+        cost = torch.empty(1, dtype=torch.int64, device="cuda")
+        ctx.solve_blocks(0 if m["mode"] == "single" else 1, torch.from_numpy(z[f"rows{k}"]).cuda(), n,
+                         types, col=col, cost=cost)
+        assert np.array_equal(col.cpu().numpy(), z[f"col{k}"].astype(np.int32)), m
+        assert int(cost.item()) == m["cost_units"], m
+    assert ctx.error_flags() == 0
+
+
 @pytest.mark.parametrize("mode,n,B", [(0, 256, 64), (0, 64, 40), (0, 100, 16), (1, 256, 8),
                                       (1, 37, 9),
                                       # large blocks (row rebuilt from the wishlist per step),

@@ -101,6 +101,22 @@ def test_santa_blocks_cost_and_assignment(santa_blocks):
         assert np.array_equal(col_f, col)
 
 
+def test_santa_blocks_reference_sizes(full_data):
+    """The reference's own block sizes: optimize_block at block_size=2000
+    (mpi_single.py:238) and optimize_block_twins at 3000 pairs
+    (mpi_twins.py:244), solved by the reference in the build container
+    (tests/golden/santa_blocks_large.npz); the oracle's round equals them."""
+    from conftest import load_npz_cases
+    z, meta = load_npz_cases("santa_blocks_large.npz")
+    for m in meta:
+        k, n = m["i"], m["n"]
+        mode = 0 if m["mode"] == "single" else 1
+        t = full_data.types.copy()
+        col, cost = oracle.round_blocks(mode, full_data.wish, t, z[f"rows{k}"][None], ng=full_data.ng)
+        assert np.array_equal(col[0], z[f"col{k}"].astype(np.int64)), m
+        assert int(cost[0]) == m["cost_units"], m
+
+
 def test_score_matches_reference(full_data):
     g = golden_json("santa_score.json")
     assert sha(full_data.wish) == g["data"]["wish_sha"], "synthetic generator drifted"

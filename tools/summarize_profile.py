@@ -22,7 +22,8 @@ def pmc(path):
 
 
 def short(name):
-    for key in ("santa_vt_kernel", "santa_sw_kernel", "santa_block_kernel", "score_kernel",
+    for key in ("santa_sp_kernel", "santa_vt_kernel", "santa_sw_kernel", "santa_block_kernel",
+                "santa_big_kernel", "score_kernel",
                 "sample_kernel", "lsap_i64_kernel", "lsap_f64_kernel"):
         if key in name:
             return key
