@@ -36,6 +36,10 @@ def main(src, tag, root):
     stats = glob.glob(os.path.join(src, "trace_kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    for part in ("fetch", "write", "sq1", "sq2", "fetch_score"):
+        f = os.path.join(src, f"{part}_counter_collection.csv")
+        if os.path.exists(f):
+            shutil.copy(f, os.path.join(prof, f"{tag}_pmc_{part}.csv"))
     trace = defaultdict(list)
     for f in glob.glob(os.path.join(src, "trace_kernel_trace.csv")):
         for r in csv.DictReader(open(f)):
