@@ -105,8 +105,10 @@ int sh_sample_blocks(uint64_t seed, uint64_t round, int lo, int count, int strid
  * Fused block round.  Replaces optimize_block (mpi_single.py:93-102) /
  * optimize_block_twins (mpi_twins.py:93-105) for B disjoint blocks at once
  * AND the apply step (mpi_single.py:142,151-152 / mpi_twins.py:154-156).
- * One workgroup per block: cost tile built in LDS from wishlist rows and the
- * current gift types, scipy-exact shortest-augmenting-path solve, then
+ * One workgroup per block: costs built on chip from wishlist rows and the
+ * current gift types (n <= 256: per-row hit lists / code tile in LDS; larger
+ * n: each Dijkstra row rebuilt from its wishlist row), scipy-exact
+ * shortest-augmenting-path solve, then
  *   types[rows[b*n+i]] = old types[rows[b*n+col[i]]]   (twins: both twins).
  * d_types int16 [nc] is updated IN PLACE (blocks must be disjoint: each block
  * reads and writes only its own children).
