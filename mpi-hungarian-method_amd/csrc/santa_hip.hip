@@ -1597,16 +1597,15 @@ __global__ __launch_bounds__(WAVE, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 
 struct SpLds {
   // persistent
-  size_t rowbuf, ctype, own, hits;
+  size_t ctype, own, hits;
   // build phase                // solve phase (aliases the build area)
-  size_t csort, thead, off;     size_t u, rem, vrow;
+  size_t csort, thead, off;     size_t u, rem, vrow, rowc;
   size_t total;
 };
 
 __host__ __device__ __forceinline__ SpLds sp_lds_layout(int ng, int cap) {
   SpLds L;
   size_t o = 0;
-  L.rowbuf = o; o += 256;                // row buffer: code of column j at byte j
   L.ctype = o;  o += 256 * 2;            // column gift types (old)
   L.own = o;    o += 256;                // code(i, i): row i's own (old) gift
   const size_t area = o;
@@ -1618,6 +1617,7 @@ __host__ __device__ __forceinline__ SpLds sp_lds_layout(int ng, int cap) {
   L.u = s;      s += 256 * 8;            // row duals
   L.rem = s;    s += 256;                // scipy's `remaining`: column at position p
   L.vrow = s;   s += 256;                // rows reached in the current Dijkstra
+  L.rowc = s;   s += (256 + 32) * 8;     // current row: C[i][j] per column (int64) + dump slots
   o = b > s ? b : s;
   L.hits = o;   // + a dump dword per lane; also the counting-sort scratch (ng x u32)
   o += r16(std::max((size_t)(cap + 2 * 64) * 2, (size_t)ng * 4));
@@ -1636,6 +1636,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
 }
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// hit-list entry (column | (code - nw1) << 8) -> its cost C = (code - nw1) << 32
+__device__ __forceinline__ uint64_t hit_cost(uint32_t e) {
+  return (uint64_t)(uint32_t)(int32_t)(int8_t)((e >> 8) & 0xFFu) << 32;
+}
 
 __device__ __forceinline__ uint64_t rfl_u64(uint64_t x) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
@@ -1650,8 +1656,6 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   const int n = a.n;
   const int cap = a.cap;
   const SpLds L = sp_lds_layout(a.ng, cap);
-  uint8_t *rowbuf = smem + L.rowbuf;
-  uint32_t *rowbuf32 = (uint32_t *)(smem + L.rowbuf);
   int16_t *ctype = (int16_t *)(smem + L.ctype);
   uint8_t *own = smem + L.own;
   uint16_t *hits = (uint16_t *)(smem + L.hits);
@@ -1662,6 +1666,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   int64_t *u_l = (int64_t *)(smem + L.u);
   uint8_t *rem = smem + L.rem;
   uint8_t *vrow = smem + L.vrow;
+  uint64_t *rowc = (uint64_t *)(smem + L.rowc);
 
   const uint64_t t0 = (a.flags & SH_FLAG_TIMING) ? wall_clock64() : 0;
   // -- rows (lane l owns rows 4l..4l+3), range check --------------------------------
@@ -1692,7 +1697,6 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   // type: start in csort | count << 8.  A type with >= 255 columns in one
   // block (never on Kaggle-shaped data) sends the block to the fallback.
   for (int t = lane; t < a.ng; t += WAVE) tcnt[t] = 0u;
-  rowbuf32[lane] = 0;
   ((uint32_t *)own)[lane] = 0;
   int myt[4];
 #pragma unroll
@@ -1872,27 +1876,41 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     offr[k] = (r < n) ? (int)((uint32_t)off[r] | ((uint32_t)off[r + 1] << 16)) : 0;
   }
   const uint64_t t1 = (a.flags & SH_FLAG_TIMING) ? wall_clock64() : 0;
-  __syncthreads();  // the build area becomes the solve area (u, rem, vrow)
+  __syncthreads();  // the build area becomes the solve area (u, rem, vrow, rowx)
   for (int r = lane; r < n; r += WAVE) u_l[r] = 0;
+  const int64_t E = a.E;
+  const u64x2 E2 = {(uint64_t)E, (uint64_t)E};
+  *(u64x2 *)(rowc + 4 * lane) = E2;
+  *(u64x2 *)(rowc + 4 * lane + 2) = E2;
 
   // -- solve ----------------------------------------------------------------------
+  // One Dijkstra step = one LDS round trip for the row's hit list, one for the
+  // expanded row, the relaxation of 4 columns per lane and a 64-bit DPP argmin.
+  // Book-keeping of step s (remove the winner from the live masks, move the
+  // last column of `remaining` into its position) is applied at the top of
+  // step s+1, in the shadow of that step's LDS reads.
   const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
-  const int64_t E = a.E;
-  uint32_t Ev = (uint32_t)E;
-  asm volatile("" : "+v"(Ev));  // the miss value as a VGPR constant
   const uint64_t BIAS = (uint64_t)KEY_BIAS;
   int64_t sb[4], W[4];  // spc + BIAS; -v   (columns 4*lane + k)
   i32x4 path, r4c, c4r;
   uint32_t lo[4];
   uint64_t LM[4];       // live (remaining) columns, wave masks
+  uint32_t lo_free[4], lo_asg[4];  // tie-break bits at the start of a Dijkstra
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
+    const int j = 4 * lane + k;
+    const int pos = n - 1 - j;
     W[k] = 0;
     path[k] = -1;
     r4c[k] = -1;
     c4r[k] = -1;
+    lo_free[k] = ((uint32_t)(1023 - pos) << 10) | (uint32_t)j;
+    lo_asg[k] = (1u << 20) | ((uint32_t)pos << 10);
   }
-  int64_t steps = 0;
+  uint32_t rem0 = 0;  // rem[p] = n - 1 - p for this lane's 4 positions
+#pragma unroll
+  for (int k = 0; k < 4; ++k) rem0 |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
+  int steps = 0;
   int fallbacks = 0;
   if (a.flags & SH_FLAG_BUILD_ONLY) {
 #pragma unroll
@@ -1902,56 +1920,62 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
       // Dijkstra set-up: remaining = [n-1 .. 0], all columns live
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int j = 4 * lane + k;
-        const int pos = n - 1 - j;
         sb[k] = INT64_MAX;
-        lo[k] = (r4c[k] < 0) ? (((uint32_t)(1023 - pos) << 10) | (uint32_t)j)
-                             : ((1u << 20) | ((uint32_t)pos << 10) | (uint32_t)r4c[k]);
-        LM[k] = __builtin_amdgcn_ballot_w64(j < n);
+        lo[k] = (r4c[k] < 0) ? lo_free[k] : (lo_asg[k] | (uint32_t)r4c[k]);
+        LM[k] = __builtin_amdgcn_ballot_w64(4 * lane + k < n);
       }
-      {
-        uint32_t rw = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) rw |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
-        ((uint32_t *)rem)[lane] = rw;  // rem[p] = n - 1 - p
-      }
+      ((uint32_t *)rem)[lane] = rem0;
       if (lane == 0) vrow[0] = (uint8_t)cur;
       int nvis = 1;
       int nrem = n;
       int64_t minVal = 0;
       int i = cur;
       int sink;
-      int mover = __builtin_amdgcn_readfirstlane((int)rem[n - 1]);  // column at the last position
+      int mover_v = 0;            // column at the last position (rem[n-1] = 0)
+      uint32_t kglo = ~0u;        // deferred: key bits of the previous winner
+      uint32_t kX = 0;            // deferred: position-key flip of the moved column
+      int kmover = -1;            //           ... and that column
       for (;;) {
         ++steps;
         // row i: hit range (registers), dual u[i] (LDS broadcast)
-        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane(offr[i & 3], i >> 2);
+        const int il = i >> 2;
+        const uint32_t o0 = (uint32_t)__builtin_amdgcn_readlane(offr[0], il);
+        const uint32_t o1 = (uint32_t)__builtin_amdgcn_readlane(offr[1], il);
+        const uint32_t o2 = (uint32_t)__builtin_amdgcn_readlane(offr[2], il);
+        const uint32_t o3 = (uint32_t)__builtin_amdgcn_readlane(offr[3], il);
+        const uint32_t o = (i & 2) ? ((i & 1) ? o3 : o2) : ((i & 1) ? o1 : o0);
         const int hs = (int)(o & 0xFFFFu), he = (int)(o >> 16);
         const uint64_t uraw = (uint64_t)u_l[i];
-        if (hs + lane < he) {
-          const uint32_t e = hits[hs + lane];
-          rowbuf[e & 0xFFu] = (uint8_t)(e >> 8);
-        }
+        const int hp = hs + lane;
+        const uint32_t e = hits[hp];  // hp < cap + 128: inside the hit area
+        // previous step's book-keeping (no LDS dependence)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) LM[k] &= ~__builtin_amdgcn_ballot_w64(lo[k] == kglo);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lo[k] ^= (4 * lane + k == kmover) ? kX : 0u;
+        // expand the row: hit columns get (code - nw1) << 32, the rest stay E
+        rowc[(hp < he) ? (int)(e & 0xFFu) : 256 + (lane & 31)] = hit_cost(e);
         if (__builtin_expect(he - hs > WAVE, 0)) {  // rows with more than 64 hits
-          for (int s = hs + WAVE + lane; s < he; s += WAVE) {
-            const uint32_t e = hits[s];
-            rowbuf[e & 0xFFu] = (uint8_t)(e >> 8);
+          for (int q = hs + WAVE + lane; q < he; q += WAVE) {
+            const uint32_t e2 = hits[q];
+            rowc[e2 & 0xFFu] = hit_cost(e2);
           }
         }
-        const uint32_t w = rowbuf32[lane];
-        rowbuf32[lane] = 0;
+        const u64x2 c01 = *(const u64x2 *)(rowc + 4 * lane);
+        const u64x2 c23 = *(const u64x2 *)(rowc + 4 * lane + 2);
+        *(u64x2 *)(rowc + 4 * lane) = E2;
+        *(u64x2 *)(rowc + 4 * lane + 2) = E2;
+        const uint64_t cc[4] = {c01[0], c01[1], c23[0], c23[1]};
         // u~[i] = u[i] - (minVal at which row i was reached) = u[i] - minVal now
         const int64_t ui = (int64_t)rfl_u64(uraw) - minVal;
         if (lane == 0) u_l[i] = ui;
-        // r + BIAS = C[i][j] - u~[i] - v[j] + BIAS;  C = code ? (code - nw1) << 32 : E
+        // r + BIAS = C[i][j] - u~[i] - v[j] + BIAS
         uint64_t bse = BIAS - (uint64_t)ui;
-        asm volatile("" : "+s"(bse));  // keep W + bse one 64-bit add
+        asm volatile("" : "+s"(bse));  // keep (W + C) + bse one 64-bit add
         uint64_t best = ~0ull;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const int32_t tb = (int32_t)(int8_t)((w >> (8 * k)) & 0xFFu);  // code - nw1, 0 = miss
-          const uint64_t hit = tb ? ((uint64_t)(uint32_t)tb << 32) : (uint64_t)Ev;
-          const uint64_t r = ((uint64_t)W[k] + bse) + hit;
+          const uint64_t r = ((uint64_t)W[k] + cc[k]) + bse;
           const bool lv = __builtin_amdgcn_inverse_ballot_w64(LM[k]);
           const bool upd = lv && ((int64_t)r < sb[k]);
           sb[k] = upd ? (int64_t)r : sb[k];
@@ -1991,26 +2015,23 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         const int pstar = assigned ? pk : 1023 - pk;
         const int last = nrem - 1;
         // the winner leaves `remaining`; the column at `last` moves to pstar
-#pragma unroll
-        for (int k = 0; k < 4; ++k) LM[k] &= ~__builtin_amdgcn_ballot_w64(lo[k] == glo);
-        if (pstar != last) {
-          const uint32_t X = (uint32_t)(last ^ pstar) << 10;
-          if (lane == 0) rem[pstar] = (uint8_t)mover;
-          const int mk = mover & 3;
-          const uint32_t Xl = (lane == (mover >> 2)) ? X : 0u;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) lo[k] ^= (mk == k) ? Xl : 0u;
-        }
+        // (applied to the registers at the top of the next step)
+        const int mover = __builtin_amdgcn_readfirstlane(mover_v);
+        kglo = glo;
+        kX = (uint32_t)(last ^ pstar) << 10;
+        kmover = mover;
+        if (lane == 0) rem[pstar] = (uint8_t)mover;  // no-op when pstar == last
         --nrem;
         if (!assigned) {
           sink = aux;
           break;
         }
-        mover = __builtin_amdgcn_readfirstlane((int)rem[last - 1]);
-        i = __builtin_amdgcn_readfirstlane(aux);
+        mover_v = rem[last - 1];  // consumed next step (latency hidden)
+        i = aux;
         if (lane == 0) vrow[nvis] = (uint8_t)i;
         ++nvis;
       }
+      // (the pending removal of the sink needs no dual update: spc = minVal)
       // dual updates: visited columns v[j] -= minVal - spc[j]; visited rows
       // u[i] = u~[i] + minVal (= u[i] + minVal - spc[col4row[i]])
 #pragma unroll

@@ -82,6 +82,7 @@ def main():
     out["state_round"] = a.state_round
     out["steps_total"] = int(steps.sum())
     out["steps_per_block"] = int(steps.sum()) / B
+    out["steps_max"] = int(steps.max())
     print(json.dumps(out))
 
 
