@@ -1931,7 +1931,6 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
       int64_t minVal = 0;
       int i = cur;
       int sink;
-      int mover_v = 0;            // column at the last position (rem[n-1] = 0)
       uint32_t kglo = ~0u;        // deferred: key bits of the previous winner
       uint32_t kX = 0;            // deferred: position-key flip of the moved column
       int kmover = -1;            //           ... and that column
@@ -1948,6 +1947,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         const uint64_t uraw = (uint64_t)u_l[i];
         const int hp = hs + lane;
         const uint32_t e = hits[hp];  // hp < cap + 128: inside the hit area
+        const int mover_v = rem[nrem - 1];  // the column at the last position
         // previous step's book-keeping (no LDS dependence)
 #pragma unroll
         for (int k = 0; k < 4; ++k) LM[k] &= ~__builtin_amdgcn_ballot_w64(lo[k] == kglo);
@@ -2026,32 +2026,46 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
           sink = aux;
           break;
         }
-        mover_v = rem[last - 1];  // consumed next step (latency hidden)
         i = aux;
         if (lane == 0) vrow[nvis] = (uint8_t)i;
         ++nvis;
       }
       // (the pending removal of the sink needs no dual update: spc = minVal)
-      // dual updates: visited columns v[j] -= minVal - spc[j]; visited rows
-      // u[i] = u~[i] + minVal (= u[i] + minVal - spc[col4row[i]])
+      // visited rows: u[i] = u~[i] + minVal (= u[i] + minVal - spc[col4row[i]]);
+      // the first 64 are read now and written back after the augmentation
+      const int r0 = vrow[lane];          // stale (but < 256) beyond nvis
+      // visited columns: v[j] -= minVal - spc[j]
+      const uint64_t mvb = (uint64_t)minVal + BIAS;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const bool visited = (4 * lane + k < n) && !((LM[k] >> lane) & 1ull);
-        if (visited) W[k] = W[k] + (minVal - (int64_t)((uint64_t)sb[k] - BIAS));
+        const uint64_t vis = ~LM[k] & __builtin_amdgcn_ballot_w64(4 * lane + k < n);
+        const int64_t d = (int64_t)(mvb - (uint64_t)sb[k]);
+        W[k] = __builtin_amdgcn_inverse_ballot_w64(vis) ? W[k] + d : W[k];
       }
-      for (int t = lane; t < nvis; t += WAVE) {
-        const int r = vrow[t];
-        u_l[r] = u_l[r] + minVal;
-      }
+      const int64_t u0 = u_l[r0];
       // augment along path[] from the sink back to cur (registers only)
       int j = sink;
       for (;;) {
-        const int pi = __builtin_amdgcn_readlane(path[j & 3], j >> 2);
-        const int t = __builtin_amdgcn_readlane(c4r[pi & 3], pi >> 2);
-        if (lane == (j >> 2)) r4c[j & 3] = pi;
-        if (lane == (pi >> 2)) c4r[pi & 3] = j;
+        const int jl = j >> 2;
+        const int p0 = __builtin_amdgcn_readlane(path[0], jl), p1 = __builtin_amdgcn_readlane(path[1], jl);
+        const int p2 = __builtin_amdgcn_readlane(path[2], jl), p3 = __builtin_amdgcn_readlane(path[3], jl);
+        const int pi = (j & 2) ? ((j & 1) ? p3 : p2) : ((j & 1) ? p1 : p0);
+        const int pl = pi >> 2;
+        const int t0 = __builtin_amdgcn_readlane(c4r[0], pl), t1 = __builtin_amdgcn_readlane(c4r[1], pl);
+        const int t2 = __builtin_amdgcn_readlane(c4r[2], pl), t3 = __builtin_amdgcn_readlane(c4r[3], pl);
+        const int t = (pi & 2) ? ((pi & 1) ? t3 : t2) : ((pi & 1) ? t1 : t0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          r4c[k] = (4 * lane + k == j) ? pi : r4c[k];
+          c4r[k] = (4 * lane + k == pi) ? j : c4r[k];
+        }
         j = t;
         if (pi == cur) break;
+      }
+      if (lane < nvis) u_l[r0] = u0 + minVal;
+      for (int q = lane + WAVE; q < nvis; q += WAVE) {
+        const int r = vrow[q];
+        u_l[r] = u_l[r] + minVal;
       }
     }
   }

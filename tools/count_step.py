@@ -12,9 +12,22 @@ b = s.index(".Lfunc_end", a)
 body = s[a:b].splitlines()
 idx = [i for i, l in enumerate(body) if "v_min_u32_dpp" in l][0]
 hdr = max(i for i in range(idx) if "Loop Header: Depth=2" in body[i])
-lab = body[hdr - 1].split(":")[0]
-end = max(i for i, l in enumerate(body) if lab in l and "branch" in l)
-seg = body[hdr:end + 1]
+lab = body[hdr - 1].split(":")[0] if body[hdr - 1].startswith(".LBB") else body[hdr].split(":")[0]
+tag = lab.lstrip(".L")  # e.g. BB5_246
+# basic blocks of the loop: the header, blocks annotated "in Loop: Header=<tag>" and
+# child-loop blocks ("Parent Loop <tag>") -- the loop may be rotated above its header
+blocks, curb = [], None
+for i, l in enumerate(body):
+    if l.startswith((".LBB", "; %bb")):
+        curb = [l, []]
+        blocks.append(curb)
+    if curb is not None:
+        curb[1].append(l)
+seg = []
+for head, lines in blocks:
+    text = "\n".join(lines[:3])
+    if head.startswith(lab + ":") or f"Header={tag} Depth=2" in text or f"Parent Loop {tag} " in text:
+        seg.extend(lines)
 ins = [l.strip() for l in seg if l.strip() and not l.strip().startswith((";", "."))]
 kinds = {"VALU": lambda l: l.startswith("v_"), "SALU": lambda l: l.startswith("s_") and not l.startswith(("s_nop", "s_waitcnt", "s_cbranch", "s_branch")),
          "branch": lambda l: l.startswith(("s_cbranch", "s_branch")), "DS": lambda l: l.startswith("ds_"),
