@@ -1611,7 +1611,7 @@ __host__ __device__ __forceinline__ SpLds sp_lds_layout(int ng, int cap) {
   const size_t area = o;
   size_t b = area;                       // build phase
   L.csort = b;  b += 272;                // columns sorted by gift type (+ pad)
-  L.thead = b;  b += r16((size_t)ng * 2);  // per type: start in csort | count << 8
+  L.thead = b;  b += r16((size_t)ng * 4);  // per type: first 3 columns | count << 24
   L.off = b;    b += r16(257 * 2);       // hit-list offsets per row
   size_t s = area;                       // solve phase
   L.u = s;      s += 256 * 8;            // row duals
@@ -1625,13 +1625,15 @@ __host__ __device__ __forceinline__ SpLds sp_lds_layout(int ng, int cap) {
   return L;
 }
 
+// Inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8 inside
+// each row of 16, then row_bcast 15/31 across rows).
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < WAVE; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, WAVE);
-    if (lane >= o) x += y;
-  }
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
   return x;
 }
 
@@ -1660,7 +1662,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   uint8_t *own = smem + L.own;
   uint16_t *hits = (uint16_t *)(smem + L.hits);
   uint8_t *csort = smem + L.csort;
-  uint16_t *thead = (uint16_t *)(smem + L.thead);
+  uint32_t *thead = (uint32_t *)(smem + L.thead);
   uint16_t *off = (uint16_t *)(smem + L.off);
   uint32_t *tcnt = (uint32_t *)(smem + L.hits);  // counting-sort scratch (hits not yet built)
   int64_t *u_l = (int64_t *)(smem + L.u);
@@ -1721,7 +1723,6 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
       const uint32_t h = tcnt[t];
       tcnt[t] = h | run;  // low half: fill cursor
       big |= (h >> 16) >= 255u;
-      thead[t] = (h >> 16) ? (uint16_t)(run | ((h >> 16) << 8)) : (uint16_t)0;  // start < 256 if present
       run += h >> 16;
     }
   }
@@ -1729,6 +1730,19 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     if (myt[k] >= 0) csort[atomicAdd(&tcnt[myt[k]], 1u) & 0xFFFFu] = (uint8_t)(4 * lane + k);
+  __syncthreads();
+  {  // per type: c0 | c1 << 8 | (count <= 3 ? c2 : start in csort) << 16 | count << 24
+    const int per = (a.ng + WAVE - 1) / WAVE;
+    const int t0s = lane * per, t1s = min(a.ng, t0s + per);
+    for (int t = t0s; t < t1s; ++t) {
+      const uint32_t h = tcnt[t];
+      const uint32_t c = h >> 16, e = (h & 0xFFFFu) - c;  // start in csort
+      const uint32_t x2 = c <= 3u ? (uint32_t)csort[e + 2] : e;
+      thead[t] = c ? ((uint32_t)csort[e] | ((uint32_t)csort[e + 1] << 8) | (x2 << 16) |
+                      (min(c, 255u) << 24))
+                   : 0u;
+    }
+  }
   __syncthreads();
   const uint64_t tc = (a.flags & SH_FLAG_TIMING) ? wall_clock64() : 0;
 
@@ -1769,22 +1783,40 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     return (int)(int16_t)(((z < 2 ? q.x : q.y) >> (16 * (z & 1))) & 0xFFFFu);
   };
   const int dump = cap + 2 * lane;
+  const int cb = qj * ncq;
+  // row s0 + qr: its child's id and own type from the owner lane
+  int ct[4];  // child id | (own type + 1) << 20 (children < 2^20, types < 1023)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ct[k] = child[k] | ((myt[k] + 1) << 20);
+  auto row_child = [&](int row, int &chd, int &mt) {
+    int x = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c2 = __shfl(ct[k], (row >> 2) & 63, WAVE);
+      x = ((row & 3) == k) ? c2 : x;
+    }
+    chd = x & 0xFFFFF;
+    mt = (x >> 20) - 1;
+  };
+  // the wishlist chunks of the next sub-round are loaded one sub-round ahead
+  uint2 qn[MAXQ];
+  int chdn, mtn;
+  row_child(qr, chdn, mtn);
+#pragma unroll
+  for (int t = 0; t < MAXQ; ++t) qn[t] = load_chunk(a.wish + (size_t)chdn * nw, cb + t);
 #pragma unroll 1
   for (int s0 = 0; s0 < n && fits; s0 += RPS) {
     const int row = s0 + qr;
     const bool lr = row < n;
-    int chd = 0, mt = -1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {  // child id / own type of `row` from its owner lane
-      const int c2 = __shfl(child[k], (row >> 2) & 63, WAVE);
-      const int t2 = __shfl(myt[k], (row >> 2) & 63, WAVE);
-      if ((row & 3) == k) { chd = c2; mt = t2; }
-    }
-    const int16_t *src = a.wish + (size_t)chd * nw;
-    const int cb = qj * ncq;
+    const int mt = mtn;
     uint2 q[MAXQ];
 #pragma unroll
-    for (int t = 0; t < MAXQ; ++t) q[t] = load_chunk(src, cb + t);
+    for (int t = 0; t < MAXQ; ++t) q[t] = qn[t];
+    if (s0 + RPS < n) {
+      row_child(s0 + RPS + qr, chdn, mtn);
+#pragma unroll
+      for (int t = 0; t < MAXQ; ++t) qn[t] = load_chunk(a.wish + (size_t)chdn * nw, cb + t);
+    }
     // count: the type's column count per wish (one batch of LDS reads)
     uint32_t hv[MAXQ][4];
     int cnt = 0;
@@ -1797,7 +1829,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         const bool ok = lr && (t < ncq) && (cb + t < nch) && (g >= 0);
         const uint32_t h = thead[ok ? g : 0];
         hv[t][z] = ok ? h : 0u;
-        cnt += (int)(hv[t][z] >> 8);
+        cnt += (int)(hv[t][z] >> 24);
         ownc = (ok && g == mt) ? (uint32_t)(4 * (cb + t) + z + 1) : ownc;
       }
     }
@@ -1810,47 +1842,35 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     const int start = base + (int)incl - cnt;
     if (lr && qj == 0) off[row] = (uint16_t)start;  // first lane of the row
     if (ownc) own[row] = (uint8_t)ownc;
-    // fill, half a quarter at a time: first read the (up to 3) columns of
-    // every wish's type in one batch, then write; surplus writes go to the
-    // lane's dump slot, types with >= 4 columns in the block are finished
-    // by the slow loop below
+    // fill straight from the type table (the first columns of each type);
+    // surplus writes go to the lane's dump slot, types with >= 4 columns in
+    // the block are finished by the slow loop below
     int p = start;
     bool many = false;
 #pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      uint32_t c3[MAXQ / 2][4];
+    for (int t = 0; t < MAXQ; ++t)
 #pragma unroll
-      for (int t = h2 * (MAXQ / 2); t < (h2 + 1) * (MAXQ / 2); ++t)
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-          const int e = (int)(hv[t][z] & 0xFFu);  // first column of the type in csort
-          c3[t - h2 * (MAXQ / 2)][z] = (uint32_t)csort[e] | ((uint32_t)csort[e + 1] << 8) |
-                                       ((uint32_t)csort[e + 2] << 16);
-        }
-#pragma unroll
-      for (int t = h2 * (MAXQ / 2); t < (h2 + 1) * (MAXQ / 2); ++t)
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-          const int cg = (int)(hv[t][z] >> 8);
-          const uint32_t cc = c3[t - h2 * (MAXQ / 2)][z];
-          const uint32_t tb = ((uint32_t)(4 * (cb + t) + z - nw) & 0xFFu) << 8;
-          hits[cg >= 1 ? p : dump] = (uint16_t)(tb | (cc & 0xFFu));
-          hits[cg >= 2 ? p + 1 : dump] = (uint16_t)(tb | ((cc >> 8) & 0xFFu));
-          hits[cg >= 3 ? p + 2 : dump] = (uint16_t)(tb | (cc >> 16));
-          many |= cg >= 4;
-          p += cg;
-        }
-    }
+      for (int z = 0; z < 4; ++z) {
+        const uint32_t h = hv[t][z];
+        const int cg = (int)(h >> 24);
+        const uint32_t tb = ((uint32_t)(4 * (cb + t) + z - nw) & 0xFFu) << 8;
+        hits[cg >= 1 ? p : dump] = (uint16_t)(tb | (h & 0xFFu));
+        hits[cg >= 2 ? p + 1 : dump] = (uint16_t)(tb | ((h >> 8) & 0xFFu));
+        hits[cg == 3 ? p + 2 : dump] = (uint16_t)(tb | ((h >> 16) & 0xFFu));
+        many |= cg >= 4;
+        p += cg;
+      }
     if (__builtin_expect(__any(many), 0)) {  // types with 4+ columns in this block
       int pp = start;
 #pragma unroll
       for (int t = 0; t < MAXQ; ++t)
 #pragma unroll
         for (int z = 0; z < 4; ++z) {
-          const int cg = (int)(hv[t][z] >> 8);
-          const int e = (int)(hv[t][z] & 0xFFu);
+          const int cg = (int)(hv[t][z] >> 24);
+          const int e = (int)((hv[t][z] >> 16) & 0xFFu);  // start in csort when cg >= 4
           const uint32_t tb = ((uint32_t)(4 * (cb + t) + z - nw) & 0xFFu) << 8;
-          for (int x = 3; x < cg; ++x) hits[pp + x] = (uint16_t)(tb | csort[e + x]);
+          if (cg >= 4)
+            for (int x = 2; x < cg; ++x) hits[pp + x] = (uint16_t)(tb | csort[e + x]);
           pp += cg;
         }
     }
@@ -1876,6 +1896,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     offr[k] = (r < n) ? (int)((uint32_t)off[r] | ((uint32_t)off[r + 1] << 16)) : 0;
   }
   const uint64_t t1 = (a.flags & SH_FLAG_TIMING) ? wall_clock64() : 0;
+  const uint64_t m1 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
   __syncthreads();  // the build area becomes the solve area (u, rem, vrow, rowx)
   for (int r = lane; r < n; r += WAVE) u_l[r] = 0;
   const int64_t E = a.E;
@@ -1892,7 +1913,8 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
   const uint64_t BIAS = (uint64_t)KEY_BIAS;
   int64_t sb[4], W[4];  // spc + BIAS; -v   (columns 4*lane + k)
-  i32x4 path, r4c, c4r;
+  i32x4 path, r4c;
+  uint32_t c4r = ~0u;   // column of row 4*lane + k in byte k (0xFF: none yet)
   uint32_t lo[4];
   uint64_t LM[4];       // live (remaining) columns, wave masks
   uint32_t lo_free[4], lo_asg[4];  // tie-break bits at the start of a Dijkstra
@@ -1903,7 +1925,6 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     W[k] = 0;
     path[k] = -1;
     r4c[k] = -1;
-    c4r[k] = -1;
     lo_free[k] = ((uint32_t)(1023 - pos) << 10) | (uint32_t)j;
     lo_asg[k] = (1u << 20) | ((uint32_t)pos << 10);
   }
@@ -1914,7 +1935,8 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   int fallbacks = 0;
   if (a.flags & SH_FLAG_BUILD_ONLY) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) c4r[k] = r4c[k] = 4 * lane + k;
+    for (int k = 0; k < 4; ++k) r4c[k] = 4 * lane + k;
+    c4r = (uint32_t)(4 * lane) * 0x01010101u + 0x03020100u;
   } else {
     for (int cur = 0; cur < n; ++cur) {
       // Dijkstra set-up: remaining = [n-1 .. 0], all columns live
@@ -2050,15 +2072,17 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         const int p0 = __builtin_amdgcn_readlane(path[0], jl), p1 = __builtin_amdgcn_readlane(path[1], jl);
         const int p2 = __builtin_amdgcn_readlane(path[2], jl), p3 = __builtin_amdgcn_readlane(path[3], jl);
         const int pi = (j & 2) ? ((j & 1) ? p3 : p2) : ((j & 1) ? p1 : p0);
-        const int pl = pi >> 2;
-        const int t0 = __builtin_amdgcn_readlane(c4r[0], pl), t1 = __builtin_amdgcn_readlane(c4r[1], pl);
-        const int t2 = __builtin_amdgcn_readlane(c4r[2], pl), t3 = __builtin_amdgcn_readlane(c4r[3], pl);
-        const int t = (pi & 2) ? ((pi & 1) ? t3 : t2) : ((pi & 1) ? t1 : t0);
+        // row pi: its previous column t leaves, j becomes its column (scalar
+        // read-modify-write of the packed byte, one writelane)
+        const int pl = pi >> 2, ps = 8 * (pi & 3);
+        const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)c4r, pl);
+        const int t = (int)((cw >> ps) & 0xFFu);
+        const uint32_t nw4 = (cw & ~(0xFFu << ps)) | ((uint32_t)j << ps);
+        // (lane select through M0: one SGPR operand per VOP3 on gfx950; nothing
+        // else in this kernel keeps a value in M0 -- checked in the ISA)
+        asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(c4r) : "s"(nw4), "s"(pl));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          r4c[k] = (4 * lane + k == j) ? pi : r4c[k];
-          c4r[k] = (4 * lane + k == pi) ? j : c4r[k];
-        }
+        for (int k = 0; k < 4; ++k) r4c[k] = (4 * lane + k == j) ? pi : r4c[k];
         j = t;
         if (pi == cur) break;
       }
@@ -2072,12 +2096,13 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   __syncthreads();
 
   const uint64_t t2 = (a.flags & SH_FLAG_TIMING) ? wall_clock64() : 0;
+  const uint64_t m2 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
   // -- outputs: lane handles rows i = 4*lane + k ------------------------------------
   int64_t cost = 0, dch = 0, dgh = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int i = 4 * lane + k;
-    const int col = c4r[k] < 0 ? 0 : c4r[k];
+    const int col = (int)((c4r >> (8 * k)) & 0xFFu);
     int64_t vq[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) vq[q] = __shfl(-W[q], col >> 2, WAVE);
@@ -2109,6 +2134,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     if (a.flags & SH_FLAG_TIMING) {
       const uint64_t t3 = wall_clock64();
       if (a.col) a.col[(size_t)b * n] = (int32_t)(tc - t0);  // column sort done
+      if (a.col && n > 1) a.col[(size_t)b * n + 1] = (int32_t)min(m2 - m1, (uint64_t)INT32_MAX);  // solve, shader cycles
       auto c21 = [](uint64_t x) { return x < 0x1FFFFFull ? x : 0x1FFFFFull; };
       a.steps[b] = (int64_t)(c21(t1 - t0) | (c21(t2 - t0) << 21) | (c21(t3 - t0) << 42));
     }
@@ -2890,7 +2916,10 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
   if (mode == SH_MODE_TWINS) return launch_santa<1, 1>(ctx, a, B, s);
   if (flags & SH_FLAG_SW_TILE) return launch_santa_sw(ctx, a, B, s);
-  if (flags & SH_FLAG_VT_TILE) return launch_santa_vt<0>(ctx, a, B, s);
+  // the sparse kernel packs child ids (< 2^20) and gift types (< 1023) in one
+  // dword during its build; other instances take the register-tile kernel
+  if ((flags & SH_FLAG_VT_TILE) || ctx->nc > (1 << 20) || ctx->ng > 1022)
+    return launch_santa_vt<0>(ctx, a, B, s);
   return launch_santa_sp(ctx, a, B, s);
 }
 

@@ -66,7 +66,9 @@ def main():
         t = base.clone()
         col = torch.zeros(B * a.n, dtype=torch.int32, device="cuda")
         ctx.solve_blocks(a.mode, rows, a.n, t, steps=steps, col=col, flags=_lib.SH_FLAG_TIMING | a.flags)
-        out["colsort_us"] = float(col.view(B, a.n)[:, 0].cpu().numpy().astype(float).mean()) / 100.0
+        cv = col.view(B, a.n).cpu().numpy().astype(float)
+        out["colsort_us"] = float(cv[:, 0].mean()) / 100.0
+        solve_cycles = cv[:, 1]
         v = steps.cpu().numpy().astype("uint64")
         ph = [(v & 0x1FFFFF), (v >> 21) & 0x1FFFFF, (v >> 42) & 0x1FFFFF]
         built, solved, done = [x.astype(float) / 100.0 for x in ph]  # us
@@ -75,6 +77,12 @@ def main():
                             "epilogue_mean": (done - solved).mean(), "total_max": done.max()}
         steps.zero_()
         ctx.solve_blocks(a.mode, rows, a.n, base.clone(), steps=steps, flags=a.flags)
+        sv = steps.cpu().numpy().astype(float)
+        wall_us = (solved - built)
+        out["timing_us"]["shader_MHz"] = float(solve_cycles.sum() / wall_us.sum())
+        out["timing_us"]["cycles_per_step"] = float(solve_cycles.sum() / sv.sum())
+        imax = int(sv.argmax())
+        out["timing_us"]["cycles_per_step_maxblock"] = float(solve_cycles[imax] / sv[imax])
     out["blocks"] = B
     out["budget"] = a.budget
     out["cap"] = cap
