@@ -135,6 +135,19 @@ def main():
     ev = []  # (start, end) events around the fused block kernel, per step
     state = {"best": None, "score": None}
 
+    # singles: every round is rescored (as the reference does), but off the
+    # critical path -- the score kernel reads a snapshot of the types on a
+    # side stream while the next round's blocks are solved (always-keep: the
+    # next round does not depend on the score).  Twins keep the synchronous
+    # keep-if-improved decision of mpi_twins.py:166-169.
+    side = torch.cuda.Stream(dev)
+    snaps = [torch.empty_like(types) for _ in range(2)]
+    snap_free = [None, None]
+    max_rounds = max(args.steps, args.warmup, 1)
+    sums_dev = torch.zeros((max_rounds, 4), dtype=torch.int64, device=dev)
+    sums_host = torch.zeros((max_rounds, 4), dtype=torch.int64).pin_memory()
+    pending = []
+
     def step(rnd: int, timed: bool):
         rows = ctx.sample_blocks(mode, n, nb, args.seed, rnd)
         if mode == _lib.SH_MODE_TWINS:
@@ -150,13 +163,38 @@ def main():
             ev.append((e0, e1))
         if world > 1:
             exchange(_Eng(ctx), w, mode, rows, n, nb, types, buffers)
+        if mode == _lib.SH_MODE_SINGLE:
+            k = rnd % 2
+            if snap_free[k] is not None:
+                stream.wait_event(snap_free[k])  # the score of round rnd-2 has read it
+            snaps[k].copy_(types)
+            ready = torch.cuda.Event()
+            ready.record(stream)
+            with torch.cuda.stream(side):
+                side.wait_event(ready)
+                ctx.score_sums_async(snaps[k], out=sums_dev[rnd])
+                sums_host[rnd].copy_(sums_dev[rnd], non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(side)
+            snap_free[k] = done
+            pending.append(rnd)
+            return
         sc, sg, _, _ = ctx.score_sums(types)  # readback every round, as the reference
         s = santa_hip.score_from_sums(sc, sg, ctx.nc, ctx.ng, ctx.n_wish, ctx.n_good)
         if state["best"] is None or s > state["best"]:
             state["best"] = s
-        elif mode == _lib.SH_MODE_TWINS:
+        else:
             types.copy_(backup)  # mpi_twins.py:166-169: keep only improvements
         state["score"] = s
+
+    def drain():  # host side of the pipelined singles scores (after a device sync)
+        for r in pending:
+            sc, sg = int(sums_host[r, 0]), int(sums_host[r, 1])
+            s = santa_hip.score_from_sums(sc, sg, ctx.nc, ctx.ng, ctx.n_wish, ctx.n_good)
+            if state["best"] is None or s > state["best"]:
+                state["best"] = s
+            state["score"] = s
+        pending.clear()
 
     class _Eng:
         def __init__(self, c):
@@ -176,6 +214,8 @@ def main():
     state["best"] = score0
     for r in range(args.warmup):
         step(r % max(args.steps, 1), False)
+    torch.cuda.synchronize()
+    pending.clear()
     types.copy_(ctx.upload_types(sd.types))
     state["best"] = score0
     score_start = score0
@@ -187,6 +227,7 @@ def main():
     for r in range(args.steps):
         step(r, True)
     torch.cuda.synchronize()
+    drain()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
