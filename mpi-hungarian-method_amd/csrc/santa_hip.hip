@@ -1640,7 +1640,11 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-// hit-list entry (column | (code - nw1) << 8) -> its cost C = (code - nw1) << 32
+// slot of column j = 4*lane + k in the row buffer: the two 16-byte halves a
+// lane reads are contiguous across lanes (conflict-free ds_read_b128)
+__device__ __forceinline__ int rowc_slot(int j) { return ((j & 2) << 6) | ((j >> 2) << 1) | (j & 1); }
+
+// hit-list entry (slot | (code - nw1) << 8) -> its cost C = (code - nw1) << 32
 __device__ __forceinline__ uint64_t hit_cost(uint32_t e) {
   return (uint64_t)(uint32_t)(int32_t)(int8_t)((e >> 8) & 0xFFu) << 32;
 }
@@ -1729,7 +1733,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 4; ++k)
-    if (myt[k] >= 0) csort[atomicAdd(&tcnt[myt[k]], 1u) & 0xFFFFu] = (uint8_t)(4 * lane + k);
+    if (myt[k] >= 0) csort[atomicAdd(&tcnt[myt[k]], 1u) & 0xFFFFu] = (uint8_t)rowc_slot(4 * lane + k);
   __syncthreads();
   {  // per type: c0 | c1 << 8 | (count <= 3 ? c2 : start in csort) << 16 | count << 24
     const int per = (a.ng + WAVE - 1) / WAVE;
@@ -1976,6 +1980,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) lo[k] ^= (4 * lane + k == kmover) ? kX : 0u;
         // expand the row: hit columns get (code - nw1) << 32, the rest stay E
+        // (hit entries carry the column's slot in rowc, see rowc_slot)
         rowc[(hp < he) ? (int)(e & 0xFFu) : 256 + (lane & 31)] = hit_cost(e);
         if (__builtin_expect(he - hs > WAVE, 0)) {  // rows with more than 64 hits
           for (int q = hs + WAVE + lane; q < he; q += WAVE) {
@@ -1983,14 +1988,14 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
             rowc[e2 & 0xFFu] = hit_cost(e2);
           }
         }
-        const u64x2 c01 = *(const u64x2 *)(rowc + 4 * lane);
-        const u64x2 c23 = *(const u64x2 *)(rowc + 4 * lane + 2);
-        *(u64x2 *)(rowc + 4 * lane) = E2;
-        *(u64x2 *)(rowc + 4 * lane + 2) = E2;
+        const u64x2 c01 = *(const u64x2 *)(rowc + 2 * lane);
+        const u64x2 c23 = *(const u64x2 *)(rowc + 128 + 2 * lane);
+        *(u64x2 *)(rowc + 2 * lane) = E2;
+        *(u64x2 *)(rowc + 128 + 2 * lane) = E2;
         const uint64_t cc[4] = {c01[0], c01[1], c23[0], c23[1]};
         // u~[i] = u[i] - (minVal at which row i was reached) = u[i] - minVal now
         const int64_t ui = (int64_t)rfl_u64(uraw) - minVal;
-        if (lane == 0) u_l[i] = ui;
+        *(lane == 0 ? (int64_t *)&u_l[i] : (int64_t *)&rowc[256 + (lane & 31)]) = ui;  // lane 0
         // r + BIAS = C[i][j] - u~[i] - v[j] + BIAS
         uint64_t bse = BIAS - (uint64_t)ui;
         asm volatile("" : "+s"(bse));  // keep (W + C) + bse one 64-bit add
@@ -1999,7 +2004,9 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         for (int k = 0; k < 4; ++k) {
           const uint64_t r = ((uint64_t)W[k] + cc[k]) + bse;
           const bool lv = __builtin_amdgcn_inverse_ballot_w64(LM[k]);
-          const bool upd = lv && ((int64_t)r < sb[k]);
+          // (a removed column never improves: r >= minVal >= its spc by dual
+          // feasibility, so `upd` needs no live mask)
+          const bool upd = (int64_t)r < sb[k];
           sb[k] = upd ? (int64_t)r : sb[k];
           path[k] = upd ? i : path[k];
           const uint32_t sh = (uint32_t)((uint64_t)sb[k] >> 32), sl = (uint32_t)sb[k];
@@ -2042,14 +2049,16 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         kglo = glo;
         kX = (uint32_t)(last ^ pstar) << 10;
         kmover = mover;
-        if (lane == 0) rem[pstar] = (uint8_t)mover;  // no-op when pstar == last
+        // one store: lane 0 rem[pstar] = mover (a no-op when pstar == last),
+        // lane 1 vrow[nvis] = aux (read only when the winner was assigned)
+        *(lane == 0 ? rem + pstar : lane == 1 ? vrow + nvis : (uint8_t *)&rowc[256] + lane) =
+            (uint8_t)(lane == 0 ? mover : aux);
         --nrem;
         if (!assigned) {
           sink = aux;
           break;
         }
         i = aux;
-        if (lane == 0) vrow[nvis] = (uint8_t)i;
         ++nvis;
       }
       // (the pending removal of the sink needs no dual update: spc = minVal)
