@@ -10,7 +10,14 @@ name = sys.argv[1]
 a = s.index(name)
 b = s.index(".Lfunc_end", a)
 body = s[a:b].splitlines()
-idx = [i for i, l in enumerate(body) if "v_min_u32_dpp" in l][0]
+dpp = [i for i, l in enumerate(body) if "v_min_u32_dpp" in l]
+# the innermost step loop: a v_min_u32_dpp inside a block annotated as a depth-2 loop
+def in_depth2(i):
+    for j in range(i, -1, -1):
+        if body[j].startswith((".LBB", "; %bb")):
+            return "Depth=2" in body[j] or "Depth=2" in body[j + 1]
+    return False
+idx = [i for i in dpp if in_depth2(i)][0]
 hdr = max(i for i in range(idx) if "Loop Header: Depth=2" in body[i])
 lab = body[hdr - 1].split(":")[0] if body[hdr - 1].startswith(".LBB") else body[hdr].split(":")[0]
 tag = lab.lstrip(".L")  # e.g. BB5_246
