@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the CPU baseline sample (rank 0, N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="test only: 'gloo' with --one-device rehearses N ranks on one GPU")
+    ap.add_argument("--one-device", action="store_true",
+                    help="test only: every rank uses cuda:0 (functional N>1 runs on a 1-GPU box)")
     return ap.parse_args()
 
 
@@ -108,7 +112,7 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
     import santa_hip
     from santa_hip import _lib
     from santa_hip import data as D
@@ -120,7 +124,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        else:
+            dist.init_process_group(args.dist_backend)
     mode = _lib.SH_MODE_SINGLE if args.mode == "single" else _lib.SH_MODE_TWINS
     n = args.n
     sd = D.synthetic(args.seed)

@@ -93,8 +93,10 @@ def exchange(engine, world: World, mode: int, rows: torch.Tensor, n: int, B: int
     """Make every rank's type vector identical after each solved its shard.
 
     Each rank packs the new types of its own blocks' rows (first twin only
-    for pairs), one all-gather concatenates the shards in rank order (padded
-    to equal size with row id -1), and every rank scatters all of them."""
+    for pairs), one all-gather concatenates the shards in rank order (each
+    padded to `per` blocks), and every rank scatters all of them.  Rank r's
+    slice starts at r*per*n, which is where its blocks start in `rows`, and
+    only trailing slots are padding, so recv[:B*n] lines up with rows[:B*n]."""
     b0, b1, per = shard_range(B, world.rank, world.size)
     cnt = per * n
     key = (cnt, world.size)
@@ -103,19 +105,12 @@ def exchange(engine, world: World, mode: int, rows: torch.Tensor, n: int, B: int
         buffers["key"] = key
         buffers["send"] = torch.full((cnt,), -1, dtype=torch.int16, device=dev)
         buffers["recv"] = torch.empty((cnt * world.size,), dtype=torch.int16, device=dev)
-        buffers["rows_all"] = torch.full((cnt * world.size,), -1, dtype=torch.int32, device=dev)
-    send, recv, rows_all = buffers["send"], buffers["recv"], buffers["rows_all"]
+    send, recv = buffers["send"], buffers["recv"]
     mine = rows[b0 * n:b1 * n]
     if mine.numel():
         engine.pack_types(types, mine, send[:mine.numel()])
     all_gather_flat(recv, send, world.group)
-    # padded layout: rank r's slots hold blocks [r*per, r*per + per) of rows
-    rows_all.fill_(-1)
-    for r in range(world.size):
-        r0, r1, _ = shard_range(B, r, world.size)
-        if r1 > r0:
-            rows_all[r * cnt: r * cnt + (r1 - r0) * n].copy_(rows[r0 * n:r1 * n])
-    engine.unpack_types(types, rows_all, recv, mode)
+    engine.unpack_types(types, rows[:B * n], recv[:B * n], mode)
 
 
 def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, n: int = 256,
