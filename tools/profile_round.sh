@@ -9,7 +9,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT -o trace --output-format csv -- \
-    python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/bench_under_trace.json
+    python3 -u bench.py --no-cpu-baseline > $OUT/bench_under_trace.json
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT -o fetch --output-format csv -- \
     python3 -u tools/probe.py --phase solve --reps 1 > $OUT/probe_fetch.json
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT -o write --output-format csv -- \

@@ -42,12 +42,26 @@ def main(src, tag, root):
             shutil.copy(f, os.path.join(prof, f"{tag}_pmc_{part}.csv"))
     trace = defaultdict(list)
     for f in glob.glob(os.path.join(src, "trace_kernel_trace.csv")):
-        for r in csv.DictReader(open(f)):
+        rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+        for r in rows:
             trace[short(r["Kernel_Name"])].append(
                 (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     out = {"tag": tag, "trace_ms": {k: {"calls": len(v), "avg_ms": sum(v) / len(v),
                                          "min_ms": min(v), "max_ms": max(v)}
                                      for k, v in trace.items()}}
+    # the bench's timed rounds: launches [warmup, warmup + steps) of the block
+    # kernel (bench.py runs `warmup` untimed rounds first, one extra launch after)
+    bj = os.path.join(src, "bench_under_trace.json")
+    if os.path.exists(bj):
+        b = json.loads(open(bj).read().strip().splitlines()[-1])
+        w, k = b["warmup"], b["steps"]
+        kn = b["roofline"]["kernel"].split(" ")[0].split("<")[0]
+        v = trace.get(kn, [])
+        if len(v) >= w + k:
+            t = v[w:w + k]
+            out["timed_window"] = {"kernel": kn, "launches": f"[{w}, {w + k})",
+                                   "avg_ms": sum(t) / len(t),
+                                   "bench_kernel_avg_ms": b["roofline"]["kernel_avg_ms"]}
     fetch = pmc(os.path.join(src, "fetch_counter_collection.csv"))
     write = pmc(os.path.join(src, "write_counter_collection.csv"))
     fscore = pmc(os.path.join(src, "fetch_score_counter_collection.csv"))
