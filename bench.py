@@ -100,12 +100,61 @@ def cpu_baseline(sd, mode: int, n: int, seconds: float):
     oracle.score_sums(sd.wish, sd.goodkids, t)  # the full rescore of each round, 1 core
     score_s = time.perf_counter() - t2
     bpsN = doneN / elN if elN > 0 else 0.0
+    sc_bps, sc_done, sc_el = scipy_baseline(sd, mode, n, min(6.0, seconds / 2), ncores, rows, lo, count,
+                                            stride, nb)
     return {"value": round(bpsN, 2), "unit": "blocks/s", "cores": ncores, "kind": "port",
             "sample": f"{doneN} blocks (n={n}, rounds of {nb}) through oracle.round_blocks "
                       f"on {ncores} threads in {elN:.1f}s; {done1} blocks on 1 core in {el1:.1f}s; "
                       f"full rescore {score_s:.2f}s per round (1 core)",
             "single_core_blocks_per_s": round(done1 / el1, 2) if el1 > 0 else None,
-            "round_blocks_per_s_incl_score": round(nb / (nb / bpsN + score_s), 2) if bpsN > 0 else None}
+            "round_blocks_per_s_incl_score": round(nb / (nb / bpsN + score_s), 2) if bpsN > 0 else None,
+            "reference_lap_blocks_per_s": round(sc_bps, 2),
+            "reference_lap_sample": f"{sc_done} blocks: the reference's float32 happiness values "
+                                    f"(mpi_single.py:213-218) gathered per block with numpy + scipy "
+                                    f"linear_sum_assignment (mpi_single.py:101) on {ncores} threads "
+                                    f"in {sc_el:.1f}s"}
+
+
+def scipy_baseline(sd, mode, n, seconds, ncores, rows, lo, count, stride, nb):
+    """Saturated-scipy comparator: the reference's own LAP
+    (scipy, which releases the GIL) on a vectorised build of the reference's
+    cost matrix, one thread per core, blocks of successive rounds applied to
+    the type vector.  Singles: C[i, j] = child_happiness[child_i][type_j];
+    twins: float32 sum of both twins' values (mpi_twins.py:97-103)."""
+    import concurrent.futures as cf
+    from scipy.optimize import linear_sum_assignment
+    from santa_hip.sampler import sample_blocks
+    miss = np.float32(1.0 / (2 * sd.n_wish))
+    vals = (-2.0 * (sd.n_wish - np.arange(sd.n_wish))).astype(np.float32)
+    types = sd.types.copy()
+
+    def table(ch):
+        T = np.full((ch.shape[0], sd.ng), miss, dtype=np.float32)
+        T[np.arange(ch.shape[0])[:, None], sd.wish[ch]] = vals
+        return T
+
+    def one(block):
+        if time.perf_counter() > deadline:
+            return 0
+        t = types[block]
+        T = table(block) if mode == 0 else table(block) + table(block + 1)
+        _, col = linear_sum_assignment(T[:, t].astype(np.float64))
+        types[block] = t[col]
+        if mode == 1:
+            types[block + 1] = t[col]
+        return 1
+
+    deadline = time.perf_counter() + seconds
+    done = 0
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(ncores) as ex:
+        rnd = 0
+        while time.perf_counter() < deadline:
+            rr = rows if rnd == 0 else sample_blocks(54321, rnd, lo, count, stride, n, nb)
+            done += sum(ex.map(one, list(rr)))
+            rnd += 1
+    el = time.perf_counter() - t0
+    return (done / el if el > 0 else 0.0), done, el
 
 
 def main():
