@@ -330,9 +330,7 @@ def main():
         "score_end": state["best"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": (("santa_sp_kernel (1-wave sparse LDS tile)" if mode == 0
-                                 else "santa_block_kernel<1,1> (4-wave LDS tile)") if n <= 256
-                                else "santa_big_kernel (row rebuilt from the wishlist)"),
+                     "kernel": _lib.SH_DESIGN_NAMES[ctx.solve_design(mode, n, max(my_blocks, 1))],
                      "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                      "algorithmic_bytes_per_block": per_block,
                      "lds": {"bytes_per_launch": lds_bytes,
@@ -344,7 +342,7 @@ def main():
     # (tools/profile_round.sh -> profiles/<tag>_summary.json; FETCH_SIZE and
     # WRITE_SIZE in separate passes, KB x 1024, on a full 3730-block round)
     prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))
-    if prof and mode == 0:
+    if prof and mode == 0 and world == 1:  # the PMC passes profile a full one-GPU round
         try:
             hb = json.load(open(prof[-1]))["hbm_bytes_per_launch"]
             kname = out["roofline"]["kernel"].split(" ")[0].split("<")[0]

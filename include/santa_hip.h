@@ -55,6 +55,16 @@ extern "C" {
 #define SH_FLAG_TIMING 64u      /* dev: the sparse kernel writes phase times
                                    (wall-clock ticks since its start, 3 x 21
                                    bits: built, solved, done) into d_steps */
+#define SH_FLAG_SP_TILE 128u    /* force the one-wave sparse kernel (the
+                                   throughput design) even for few blocks  */
+
+/* Kernel designs sh_solve_blocks can dispatch to (sh_solve_design).        */
+#define SH_DESIGN_SPARSE 0   /* one wave per block, hit lists in LDS        */
+#define SH_DESIGN_LDS_TILE 1 /* 4 waves per block, byte tile in LDS         */
+#define SH_DESIGN_SW_TILE 2  /* one wave, register tile (A/B only)          */
+#define SH_DESIGN_VT_TILE 3  /* 4 waves, register tile (A/B; nc > 2^20)     */
+#define SH_DESIGN_TWINS 4    /* twins n <= 256: 4 waves, code-pair tile     */
+#define SH_DESIGN_LARGE 5    /* n > 256: row rebuilt from the wishlist      */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024
@@ -124,6 +134,15 @@ int sh_sample_blocks(uint64_t seed, uint64_t round, int lo, int count, int strid
 int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B,
                     int16_t *d_types, int32_t *d_col, int64_t *d_cost,
                     int64_t *d_delta, int64_t *d_steps, unsigned flags, void *stream);
+
+/* The kernel design sh_solve_blocks uses for these arguments (SH_DESIGN_*),
+ * or < 0 on bad arguments.  Singles n <= 256 default to the sparse kernel
+ * (highest throughput: 8 blocks per CU); when the launch has no more blocks
+ * than the device holds LDS-tile blocks at once (e.g. one GPU's shard of a
+ * round at 8 GPUs) the 4-wave LDS-tile kernel is used instead: lower
+ * latency per block, and the round time is then one block's latency.
+ * Identical results either way.                                            */
+int sh_solve_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags);
 
 /* ---------------------------------------------------------------------------
  * Score sums.  Replaces avg_normalized_happiness (mpi_single.py:13-83):

@@ -2651,6 +2651,8 @@ struct sh_ctx {
   int32_t *d_ovf = nullptr;
   int ovf_cap = 0;
   int ovf_par = 0;
+  int n_cu = 0;          // compute units (LDS-tile slot count)
+  int lds_slots = 0, lds_slots_n = -1;  // cached lds_tile_slots for one n
 };
 
 namespace {
@@ -2757,6 +2759,8 @@ int sh_ctx_create(sh_ctx **out, int device, const int16_t *h_wish, int n_wish,
   if ((e = hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device)) != hipSuccess)
     return cleanup(fail(SH_ERR_HIP, hipGetErrorString(e)));
   ctx->max_lds = lds;
+  if ((e = hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
+    return cleanup(fail(SH_ERR_HIP, hipGetErrorString(e)));
   *out = ctx;
   return SH_OK;
 }
@@ -2898,6 +2902,45 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
 }
 }  // namespace
 
+namespace {
+// LDS-tile blocks (singles, 4 waves) the device holds at once for this n.
+int lds_tile_slots(sh_ctx *ctx, int n) {
+  if (ctx->lds_slots_n == n) return ctx->lds_slots;
+  const SantaLds L = santa_lds_layout(n, 0, ctx->ng);
+  int per_cu = 0;
+  if (L.total <= 160 * 1024) {
+    if (L.total > 64 * 1024)
+      (void)hipFuncSetAttribute((const void *)santa_block_kernel<1, 0>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, santa_block_kernel<1, 0>, SANTA_WG,
+                                                     L.total) != hipSuccess)
+      per_cu = 0;
+  }
+  ctx->lds_slots = per_cu * ctx->n_cu;
+  ctx->lds_slots_n = n;
+  return ctx->lds_slots;
+}
+
+int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
+  if (n > 256) return SH_DESIGN_LARGE;
+  // twins keep the LDS tile: their 128-dword register column does not stay
+  // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
+  if (mode == SH_MODE_TWINS) return SH_DESIGN_TWINS;
+  if (flags & SH_FLAG_LDS_TILE) return SH_DESIGN_LDS_TILE;
+  if (flags & SH_FLAG_SW_TILE) return SH_DESIGN_SW_TILE;
+  // the sparse kernel packs child ids (< 2^20) and gift types (< 1023) in one
+  // dword during its build; other instances take the register-tile kernel
+  if ((flags & SH_FLAG_VT_TILE) || ctx->nc > (1 << 20) || ctx->ng > 1022) return SH_DESIGN_VT_TILE;
+  if (flags & SH_FLAG_SP_TILE) return SH_DESIGN_SPARSE;
+  // few blocks (at most one resident wave of LDS-tile blocks): every block
+  // starts at once and the launch takes one block's latency, which the
+  // 4-wave tile kernel has lower (MI355X, one GPU's shard of a round at 8
+  // GPUs, 466 blocks: 2.25 vs 2.41 ms at round 0, 0.81 vs 0.95 ms at round 10)
+  if (B <= lds_tile_slots(ctx, n)) return SH_DESIGN_LDS_TILE;
+  return SH_DESIGN_SPARSE;
+}
+}  // namespace
+
 extern "C" {
 
 int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, int16_t *d_types,
@@ -2917,19 +2960,22 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   a.cap = 0; a.ovf_cnt = nullptr; a.ovf_list = nullptr;
   a.blist = nullptr; a.bcount = nullptr; a.ovf_reset = nullptr;
   hipStream_t s = (hipStream_t)stream;
-  if (n > 256)
-    return mode == SH_MODE_SINGLE ? launch_santa_big<0>(ctx, a, B, s) : launch_santa_big<1>(ctx, a, B, s);
-  if (flags & SH_FLAG_LDS_TILE)
-    return mode == SH_MODE_SINGLE ? launch_santa<1, 0>(ctx, a, B, s) : launch_santa<1, 1>(ctx, a, B, s);
-  // twins keep the LDS tile: their 128-dword register column does not stay
-  // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
-  if (mode == SH_MODE_TWINS) return launch_santa<1, 1>(ctx, a, B, s);
-  if (flags & SH_FLAG_SW_TILE) return launch_santa_sw(ctx, a, B, s);
-  // the sparse kernel packs child ids (< 2^20) and gift types (< 1023) in one
-  // dword during its build; other instances take the register-tile kernel
-  if ((flags & SH_FLAG_VT_TILE) || ctx->nc > (1 << 20) || ctx->ng > 1022)
-    return launch_santa_vt<0>(ctx, a, B, s);
-  return launch_santa_sp(ctx, a, B, s);
+  switch (pick_design(ctx, mode, n, B, flags)) {
+    case SH_DESIGN_LARGE:
+      return mode == SH_MODE_SINGLE ? launch_santa_big<0>(ctx, a, B, s) : launch_santa_big<1>(ctx, a, B, s);
+    case SH_DESIGN_TWINS: return launch_santa<1, 1>(ctx, a, B, s);
+    case SH_DESIGN_LDS_TILE: return launch_santa<1, 0>(ctx, a, B, s);
+    case SH_DESIGN_SW_TILE: return launch_santa_sw(ctx, a, B, s);
+    case SH_DESIGN_VT_TILE: return launch_santa_vt<0>(ctx, a, B, s);
+    default: return launch_santa_sp(ctx, a, B, s);
+  }
+}
+
+int sh_solve_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
+  if (!ctx) return fail(SH_ERR_ARGS, "null ctx");
+  if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS) return fail(SH_ERR_ARGS, "bad mode");
+  if (n <= 0 || n > SH_MAX_N_SANTA || B < 0) return fail(SH_ERR_ARGS, "bad n or B");
+  return pick_design(ctx, mode, n, B, flags);
 }
 
 int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream) {

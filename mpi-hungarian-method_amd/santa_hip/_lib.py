@@ -25,6 +25,11 @@ SH_FLAG_LDS_TILE = 8
 SH_FLAG_SW_TILE = 16
 SH_FLAG_VT_TILE = 32
 SH_FLAG_TIMING = 64
+SH_FLAG_SP_TILE = 128
+SH_DESIGN_NAMES = {0: "santa_sp_kernel (1-wave sparse LDS tile)", 1: "santa_block_kernel (4-wave LDS byte tile)",
+                   2: "santa_sw_kernel (1-wave register tile)", 3: "santa_vt_kernel (4-wave register tile)",
+                   4: "santa_block_kernel (twins, 4-wave code-pair tile)",
+                   5: "santa_big_kernel (row rebuilt from the wishlist)"}
 SH_MAX_N = 1024
 SH_MAX_N_SANTA = 4096
 
@@ -45,6 +50,7 @@ SIGNATURES = {
     "sh_score": (_I, [_P, _P, _P, _P]),
     "sh_ctx_error_flags": (_I, [_P, _P]),
     "sh_ctx_fallback_steps": (_I, [_P, _P]),
+    "sh_solve_design": (_I, [_P, _I, _I, _I, _U]),
     "sh_ctx_set_sparse_budget": (_I, [_P, _I]),
     "sh_pack_types": (_I, [_P, _P, _I, _P, _P]),
     "sh_unpack_types": (_I, [_P, _P, _I, _P, _I, _P]),

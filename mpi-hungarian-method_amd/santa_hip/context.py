@@ -121,6 +121,11 @@ class SantaGPU:
                                         _lib.SH_COMPAT_TIEBREAK | flags, self.stream)
         _lib.check(rc, "sh_solve_blocks")
 
+    def solve_design(self, mode: int, n: int, B: int, flags: int = 0) -> int:
+        """The kernel design (SH_DESIGN_*) solve_blocks dispatches to."""
+        rc = _lib.lib().sh_solve_design(self._h, mode, n, B, _lib.SH_COMPAT_TIEBREAK | flags)
+        return _lib.check(rc, "sh_solve_design")
+
     def error_flags(self) -> int:
         return _lib.check(_lib.lib().sh_ctx_error_flags(self._h, self.stream), "sh_ctx_error_flags")
 

@@ -138,25 +138,29 @@ def test_santa_blocks_golden_reference_sizes(sh, ctx, full_data):
 def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
     """Fused build+solve+apply on the GPU equals the CPU oracle: col, exact
     cost, the whole new type vector, and the happiness deltas."""
+    from santa_hip import _lib
     rows = ctx.sample_blocks(mode, n, B, 2024, 1)
-    types = ctx.upload_types(full_data.types)
-    col = torch.empty(B * n, dtype=torch.int32, device="cuda")
-    cost = torch.empty(B, dtype=torch.int64, device="cuda")
-    delta = torch.zeros(2, dtype=torch.int64, device="cuda")
-    steps = torch.empty(B, dtype=torch.int64, device="cuda")
-    ctx.solve_blocks(mode, rows, n, types, col=col, cost=cost, delta=delta, steps=steps)
     t_host = full_data.types.copy()
     st = np.zeros(2, dtype=np.uint64)
     ocol, ocost = oracle.round_blocks(mode, full_data.wish, t_host, rows.cpu().numpy().reshape(B, n),
                                       stats=st, ng=full_data.ng)
-    assert np.array_equal(col.cpu().numpy().reshape(B, n), ocol)
-    assert np.array_equal(cost.cpu().numpy(), ocost)
-    assert np.array_equal(types.cpu().numpy(), t_host)
-    assert int(steps.sum()) == int(st[0])
     s0 = oracle.score_sums(full_data.wish, full_data.goodkids, full_data.types)
     s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
-    assert delta.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]]
-    assert ctx.error_flags() == 0
+    # singles n <= 256: the default for few blocks (LDS tile) and the forced
+    # throughput kernel (sparse) are both checked
+    for fl in ((0, _lib.SH_FLAG_SP_TILE) if mode == 0 and n <= 256 else (0,)):
+        types = ctx.upload_types(full_data.types)
+        col = torch.empty(B * n, dtype=torch.int32, device="cuda")
+        cost = torch.empty(B, dtype=torch.int64, device="cuda")
+        delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+        steps = torch.empty(B, dtype=torch.int64, device="cuda")
+        ctx.solve_blocks(mode, rows, n, types, col=col, cost=cost, delta=delta, steps=steps, flags=fl)
+        assert np.array_equal(col.cpu().numpy().reshape(B, n), ocol), fl
+        assert np.array_equal(cost.cpu().numpy(), ocost), fl
+        assert np.array_equal(types.cpu().numpy(), t_host), fl
+        assert int(steps.sum()) == int(st[0]), fl
+        assert delta.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]], fl
+        assert ctx.error_flags() == 0
 
 
 def test_full_round_properties(sh, ctx, full_data):
@@ -382,7 +386,7 @@ def test_sparse_overflow_fallback(sh, ctx, full_data):
         for budget in (6000, 16500, 17500, 0, 0, 4096, 0):
             cap = ctx.set_sparse_budget(budget)
             assert cap >= 0
-            got = _round_outputs(ctx, full_data, 0, rows, nn, B)
+            got = _round_outputs(ctx, full_data, 0, rows, nn, B, _lib.SH_FLAG_SP_TILE)
             for x, y in zip(want, got):
                 assert np.array_equal(x, y), budget
         assert ctx.error_flags() == 0
@@ -391,7 +395,7 @@ def test_sparse_overflow_fallback(sh, ctx, full_data):
 
 
 def test_kernel_designs_agree(sh, ctx, full_data):
-    """The one-wave sparse-tile kernel (default for singles), the 4-wave
+    """The one-wave sparse-tile kernel (SH_FLAG_SP_TILE), the default dispatch, the 4-wave
     register-tile kernel (SH_FLAG_VT_TILE), the one-wave register kernel
     (SH_FLAG_SW_TILE) and the 4-wave LDS-tile kernel (SH_FLAG_LDS_TILE)
     produce identical rounds: col, cost, deltas, steps, state."""
@@ -400,7 +404,8 @@ def test_kernel_designs_agree(sh, ctx, full_data):
     for B, nn in ((64, 256), (16, 100), (8, 37), (8, 130), (4, 1), (6, 255), (5, 64)):
         rows = ctx.sample_blocks(mode, nn, B, 77, 9)
         outs = []
-        for fl in (0, _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_SW_TILE, _lib.SH_FLAG_LDS_TILE):
+        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_SW_TILE,
+                   _lib.SH_FLAG_LDS_TILE):
             types = ctx.upload_types(full_data.types)
             col = torch.empty(B * nn, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -412,3 +417,18 @@ def test_kernel_designs_agree(sh, ctx, full_data):
         for other in outs[1:]:
             for x, y in zip(outs[0], other):
                 assert np.array_equal(x, y), (B, nn)
+
+
+def test_design_dispatch(sh, ctx):
+    """Singles n=256: the sparse kernel for a full round (3730 blocks), the
+    4-wave LDS tile when the launch fits in one resident wave of LDS-tile
+    blocks (one GPU's shard at 8 GPUs: 466), the sparse kernel again when
+    forced; twins and large blocks have one design each."""
+    from santa_hip import _lib
+    assert ctx.solve_design(0, 256, 3730) == 0
+    assert ctx.solve_design(0, 256, 466) == 1
+    assert ctx.solve_design(0, 256, 466, _lib.SH_FLAG_SP_TILE) == 0
+    assert ctx.solve_design(0, 256, 933) == 0
+    assert ctx.solve_design(1, 256, 78) == 4
+    assert ctx.solve_design(0, 2000, 477) == 5
+    assert ctx.solve_design(1, 3000, 6) == 5
