@@ -54,13 +54,12 @@ def shard_range(B: int, rank: int, size: int) -> tuple[int, int, int]:
 
 def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
     """Rank-ordered concatenation of every rank's `inp` into `out` (RCCL
-    all-gather on GPUs; gloo, which has no int16, gathers an int32 copy)."""
+    all-gather over xGMI on GPUs).  An all-gather only moves bytes, and
+    neither torch's NCCL/RCCL process group nor gloo maps int16, so int16
+    buffers travel as their uint8 bytes (no copy, same HBM bytes)."""
     import torch.distributed as dist
-    if inp.dtype == torch.int16 and dist.get_backend(group) == "gloo":
-        o32 = torch.empty(out.shape, dtype=torch.int32, device=out.device)
-        all_gather_flat(o32, inp.to(torch.int32), group)
-        out.copy_(o32)
-        return
+    if inp.dtype == torch.int16:
+        inp, out = inp.contiguous().view(torch.uint8), out.view(torch.uint8)
     try:
         dist.all_gather_into_tensor(out, inp, group=group)
     except (RuntimeError, AttributeError, NotImplementedError):

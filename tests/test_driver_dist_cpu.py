@@ -91,3 +91,21 @@ def test_twins_rank_limit_matches_reference():
     with pytest.raises(ValueError):
         run_rounds(eng, torch.from_numpy(sd.types.copy()), mode=_lib.SH_MODE_TWINS, n=64,
                    blocks_per_round=1, world=World(0, nb + 1, None), max_rounds=1)
+
+
+def test_all_gather_sends_rccl_dtypes(monkeypatch):
+    """torch's NCCL/RCCL process group has no int16 datatype: the int16 type
+    vectors must reach the collective as bytes (uint8), not as int16."""
+    from santa_hip.driver import all_gather_flat
+    seen = []
+
+    def fake(out, inp, group=None):
+        seen.append((out.dtype, inp.dtype))
+        out.copy_(inp.repeat(out.numel() // inp.numel()))
+
+    monkeypatch.setattr(dist, "all_gather_into_tensor", fake)
+    inp = torch.arange(-5, 5, dtype=torch.int16)
+    out = torch.empty(20, dtype=torch.int16)
+    all_gather_flat(out, inp)
+    assert seen == [(torch.uint8, torch.uint8)]
+    assert torch.equal(out, torch.cat([inp, inp]))

@@ -432,3 +432,35 @@ def test_design_dispatch(sh, ctx):
     assert ctx.solve_design(1, 256, 78) == 4
     assert ctx.solve_design(0, 2000, 477) == 5
     assert ctx.solve_design(1, 3000, 6) == 5
+
+
+# --------------------------------------------------------------------------- RCCL exchange
+def test_exchange_over_rccl(sh, ctx, full_data):
+    """The per-round exchange (pack -> all-gather -> unpack) through a real
+    RCCL process group (one rank: this box has one GPU; the N>1 logic is
+    covered by the gloo tests).  Catches dtypes RCCL does not carry."""
+    import socket
+
+    import torch.distributed as dist
+    from santa_hip.driver import GPUEngine, World, exchange
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        for mode, n in ((0, 256), (1, 64)):
+            _, _, _, nb = ctx.geometry(mode, n)
+            rows = ctx.sample_blocks(mode, n, nb, 7, 1)
+            types = ctx.upload_types(full_data.types)
+            ctx.solve_blocks(mode, rows, n, types)
+            want = types.clone()
+            bufs = {}
+            exchange(GPUEngine(ctx), World(0, 1, None), mode, rows, n, nb, types, bufs)
+            torch.cuda.synchronize()
+            # the all-gathered bytes are this rank's packed new types
+            assert torch.equal(bufs["recv"][:rows.numel()], want[rows.long()]), mode
+            assert torch.equal(types, want), mode
+    finally:
+        dist.destroy_process_group()
