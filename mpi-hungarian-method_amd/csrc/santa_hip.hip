@@ -454,9 +454,13 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
       } else {
         minVal = minVal + ((int64_t)hi - BIAS);
       }
-      const bool assigned = (g >> (2 * FB)) & 1u;
-      const int pk = (int)((g >> FB) & FM);
-      const int aux = (int)(g & FM);
+      // decode the winner in SGPRs: the next row index then addresses the
+      // tile and u[] with scalar arithmetic (no per-lane multiply)
+      uint32_t glo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+      asm volatile("" : "+s"(glo));
+      const bool assigned = (glo >> (2 * FB)) & 1u;
+      const int pk = (int)((glo >> FB) & FM);
+      const int aux = (int)(glo & FM);
       const int pstar = assigned ? pk : (int)FM - pk;
       const int last = nrem - 1;
 #pragma unroll
@@ -518,18 +522,39 @@ struct TileU8Loader {  // singles: uint8 rank codes, row stride RS bytes
   }
 };
 
+constexpr int TWIN_LUT = 1024;  // 3 classes x 256, padded to the 10-bit index mask
 template <int NW, int K>
-struct TileU16Loader {  // twins: uint16 code pairs, row stride RS elements
+struct TileU16Loader {  // twins: uint16 cost-table indices, row stride RS elements
   const uint16_t *tile;
-  int RS, nw1;
-  int64_t E;
+  const int64_t *lut;  // twin_lut_index -> exact cost (units), in LDS
+  int RS;
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint16_t *p = tile + (size_t)i * RS + w * (WAVE * K) + lane;
 #pragma unroll
-    for (int k = 0; k < K; ++k) c[k] = twin_cost(p[k * WAVE], nw1, E);
+    for (int k = 0; k < K; ++k) c[k] = lut[p[k * WAVE] & (TWIN_LUT - 1)];  // (lanes past n read any row)
   }
 };
+
+// Twins tile entries in the 4-wave kernel are re-coded after the build from
+// the code pair (c1 | c2 << 8) to idx = cls << 8 | a (cls = number of twins
+// wishing the column's gift, a = a1 + a2), so a Dijkstra step decodes a cost
+// with one LDS table read instead of the float32-rounding arithmetic of
+// twin_cost.  The table holds twin_cost of every (cls, a).
+__device__ __forceinline__ uint32_t twin_lut_index(uint32_t code16, int nw1) {
+  const uint32_t c1 = code16 & 0xFFu, c2 = code16 >> 8;
+  const uint32_t a = (c1 ? nw1 - c1 : 0u) + (c2 ? nw1 - c2 : 0u);
+  return ((uint32_t)(c1 != 0) + (uint32_t)(c2 != 0)) << 8 | a;
+}
+__device__ __forceinline__ int64_t twin_lut_cost(uint32_t idx, int64_t E) {
+  const int cls = (int)(idx >> 8), a = (int)(idx & 0xFFu);
+  const int64_t m = cls == 2 ? 0 : (cls == 1 ? one_hit_residual(a, E) : 2 * E);
+  return (int64_t)(-a) * 4294967296LL + m;
+}
+// child-side happiness of both twins: 2a (both wish), 2a - 1 (one), -2 (none)
+__device__ __forceinline__ int64_t twin_lut_happy(uint32_t idx) {
+  return 2 * (int64_t)(idx & 0xFFu) - (2 - (int64_t)(idx >> 8));
+}
 
 template <int NW, int K, typename S>
 struct GlobalLoader {  // generic LSAP: rows streamed from global memory
@@ -614,7 +639,7 @@ constexpr int SANTA_NW = 4;
 constexpr int SANTA_WG = SANTA_NW * WAVE;
 
 struct SantaLds {
-  size_t tile, u, rows, ctype, c4r, r4c, path, red, head, nxt, part, total;
+  size_t tile, u, rows, ctype, c4r, r4c, path, red, head, nxt, part, lut, total;
   int RS;
 };
 
@@ -633,6 +658,7 @@ __host__ __device__ __forceinline__ SantaLds santa_lds_layout(int n, int mode, i
   L.head = off;  off += r16((size_t)ng * 4);
   L.nxt = off;   off += r16((size_t)n * 2);
   L.part = off;  off += r16((size_t)SANTA_NW * 3 * 8);
+  L.lut = off;   off += mode ? (size_t)TWIN_LUT * 8 : 0;
   L.total = off;
   return L;
 }
@@ -742,11 +768,19 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
     S.c4r[i] = -1;
     S.r4c[i] = -1;
   }
+  const int nw1 = a.n_wish + 1;
+  int64_t *lut = (int64_t *)(smem + L.lut);
+  if (MODE) {  // code pairs -> cost-table indices (see twin_lut_index)
+    for (int q = tid; q < TWIN_LUT; q += SANTA_WG) lut[q] = twin_lut_cost((uint32_t)q, a.E);
+    __syncthreads();
+    uint16_t *t16 = (uint16_t *)tile8;
+    const int cnt = n * RS;
+    for (int q = tid; q < cnt; q += SANTA_WG) t16[q] = (uint16_t)twin_lut_index(t16[q], nw1);
+  }
   __syncthreads();
   // -- solve ------------------------------------------------------------------
   int64_t steps = 0;
   int fallbacks = 0;
-  const int nw1 = a.n_wish + 1;
   const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
   if (a.flags & SH_FLAG_BUILD_ONLY) {  // phase timing: tile build + apply identity
     for (int i = tid; i < n; i += SANTA_WG) S.c4r[i] = (int16_t)i;
@@ -755,7 +789,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
     const TileU8Loader<SANTA_NW, K> ld{tile8, RS, nw1, a.E};
     sap_solve_mw<SANTA_NW, K>(n, ld, S, steps, fallbacks, exact);
   } else {
-    const TileU16Loader<SANTA_NW, K> ld{(const uint16_t *)tile8, RS, nw1, a.E};
+    const TileU16Loader<SANTA_NW, K> ld{(const uint16_t *)tile8, lut, RS};
     sap_solve_mw<SANTA_NW, K>(n, ld, S, steps, fallbacks, exact);
   }
   // -- outputs: col, exact cost, happiness deltas, apply ---------------------
@@ -775,9 +809,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
       const uint16_t *t16 = (const uint16_t *)tile8;
       const uint32_t cn = t16[(size_t)i * RS + col];
       const uint32_t co = t16[(size_t)i * RS + i];
-      cost += twin_cost(cn, nw1, a.E);
-      dch += child_happy(cn & 0xFF, nw1) + child_happy(cn >> 8, nw1) -
-             child_happy(co & 0xFF, nw1) - child_happy(co >> 8, nw1);
+      cost += lut[cn & (TWIN_LUT - 1)];
+      dch += twin_lut_happy(cn) - twin_lut_happy(co);
       dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
              gift_happy(a, child, told) - gift_happy(a, child + 1, told);
     }
