@@ -332,9 +332,20 @@ __device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t x) {
 
 // 64-bit unsigned min as two fused 32-bit reductions (high word, then the
 // low word among the lanes holding the minimal high word).
+// UNIQ: when one lane holds the minimal high word, read the low word from
+// that lane instead of a second reduction (1-2 % per step for the
+// latency-bound multi-wave solver; the branch costs the one-wave sparse
+// kernel 7 % at full occupancy, so it keeps the plain two passes).
+template <bool UNIQ = false>
 __device__ __forceinline__ uint64_t wave_min_u64_fast(uint64_t x) {
   const uint32_t h = (uint32_t)(x >> 32);
   const uint32_t mh = wave_min_u32_dpp(h);
+  if constexpr (UNIQ) {
+    const uint64_t tie = __builtin_amdgcn_ballot_w64(h == mh);
+    if (__builtin_popcountll(tie) == 1)
+      return ((uint64_t)mh << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)__builtin_ctzll(tie));
+  }
   const uint32_t ml = wave_min_u32_dpp(h == mh ? (uint32_t)x : 0xFFFFFFFFu);
   return ((uint64_t)mh << 32) | ml;
 }
@@ -429,7 +440,7 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
         const uint64_t key = (kh << LOB) | lo_of(k, j);
         best = umin64(best, act ? key : ~0ull);
       }
-      uint64_t g = block_min_u64<NW>(wave_min_u64_fast(best), S.red + par * NW, w);
+      uint64_t g = block_min_u64<NW>(wave_min_u64_fast<true>(best), S.red + par * NW, w);
       g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
       par ^= 1;
