@@ -390,12 +390,15 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
   // key fields: FB bits of position and of row/column (n <= 2^FB), 1 class bit
   constexpr int LOB = 2 * FB + 1;
   constexpr uint32_t FM = (1u << FB) - 1u;
-  constexpr uint64_t HI_MAX = (1ull << (64 - LOB)) - 1;
+  constexpr uint32_t SHM = (1u << (32 - LOB)) - 1u;  // high-word clamp of sb
+  constexpr uint32_t SAT = SHM << LOB;                // key high words >= SAT: saturated
+  constexpr uint32_t LOW = 1u << LOB;                 // key high words < LOW: sb < 2^32
   constexpr int64_t BIAS = 1ll << (63 - LOB);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t INF = INT64_MAX;
   int64_t spc[K], nv[K];  // nv = -v (column duals, negated)
   int path[K], pos[K], r4c[K];
+  uint32_t lo[K];  // tie-break bits of the column (cached; the mover's flip per step)
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     nv[k] = 0;
@@ -414,6 +417,7 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
       spc[k] = INF;
       pos[k] = (j < n) ? (n - 1 - j) : -1;
       r4c[k] = (j < n) ? S.r4c[j] : -1;
+      lo[k] = lo_of(k, j);
     }
     int nrem = n;
     int64_t minVal = 0;
@@ -429,23 +433,30 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
       uint64_t best = ~0ull;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const int j = w * (WAVE * K) + k * WAVE + lane;
         const bool act = pos[k] >= 0;
         const int64_t r = c[k] + kU + nv[k];
         const bool upd = act && (r < spc[k]);
         spc[k] = upd ? r : spc[k];
         path[k] = upd ? i : path[k];
+        // key = (sb << LOB) | lo with sb = spc - minVal + BIAS.  The high word
+        // of sb is clamped to [0, SHM] (one med3): sb >= 2^(64-LOB) - 2^32
+        // gives key high words >= SAT, sb < 2^32 (including sb < 0: the first
+        // step of a Dijkstra can relax below minVal = 0 when C < v) gives
+        // high words < 2^LOB, below every other key; a winner in either band
+        // is re-decided by the exact argmin below
         const uint64_t sb = (uint64_t)spc[k] + kb;
-        const uint64_t kh = (sb <= HI_MAX) ? sb : (((int64_t)sb < 0) ? 0 : HI_MAX);
-        const uint64_t key = (kh << LOB) | lo_of(k, j);
-        best = umin64(best, act ? key : ~0ull);
+        const uint32_t sh = (uint32_t)(sb >> 32), sl = (uint32_t)sb;
+        const uint32_t shc = (uint32_t)min(max((int)sh, 0), (int)SHM);
+        const uint32_t kh = __builtin_amdgcn_alignbit(shc, sl, 32 - LOB);
+        const uint64_t key = ((uint64_t)kh << 32) | ((sl << LOB) | lo[k]);
+        best = (act && key < best) ? key : best;
       }
       uint64_t g = block_min_u64<NW>(wave_min_u64_fast<true>(best), S.red + par * NW, w);
       g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
       par ^= 1;
       const uint64_t hi = g >> LOB;
-      if (exact || hi == 0 || hi == HI_MAX) {
+      if (exact || (uint32_t)(g >> 32) - LOW >= SAT - LOW) {
         // exact two-pass argmin: min spc (signed), then min key-low among ties
         uint64_t m = ~0ull;
 #pragma unroll
@@ -456,8 +467,7 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
         uint64_t b2 = ~0ull;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          const int j = w * (WAVE * K) + k * WAVE + lane;
-          if (pos[k] >= 0 && spc[k] == ms) b2 = umin64(b2, lo_of(k, j));
+          if (pos[k] >= 0 && spc[k] == ms) b2 = umin64(b2, lo[k]);
         }
         g = block_min_u64<NW>(wave_min_u64_dpp(b2), S.red + 3 * NW, w);
         minVal = ms;
@@ -474,9 +484,11 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
       const int aux = (int)(glo & FM);
       const int pstar = assigned ? pk : (int)FM - pk;
       const int last = nrem - 1;
+      const uint32_t kX = (uint32_t)(last ^ pstar) << FB;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const int p = pos[k];
+        lo[k] ^= (p == last) ? kX : 0u;  // the mover's position key
         pos[k] = (p == pstar) ? -1 : ((p == last) ? pstar : p);
       }
       --nrem;

@@ -3,7 +3,7 @@ usage: python tools/count_step.py <kernel-substring> [--dump]"""
 import subprocess, sys
 src = "mpi-hungarian-method_amd/csrc/santa_hip.hip"
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
-                "-Iinclude", "--cuda-device-only", "-S", "-o", "/tmp/sh.s", src], check=True,
+                "-Iinclude"] + [x for x in __import__("os").environ.get("SH_DEFS","").split() if x] + ["--cuda-device-only", "-S", "-o", "/tmp/sh.s", src], check=True,
                stderr=subprocess.DEVNULL)
 s = open("/tmp/sh.s").read()
 name = sys.argv[1]
