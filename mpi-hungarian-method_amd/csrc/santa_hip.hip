@@ -367,7 +367,7 @@ struct SolveLds {
   int16_t *c4r;     // [n]   col4row (the result)
   int16_t *r4c;     // [n]   row4col
   int16_t *path;    // [n]   path dump of the visited columns
-  uint64_t *red;    // [2 * NW + 2 * NW]  step partials (double-buffered) + fallback
+  uint64_t *red;    // [4 * NW]  step argmin words (3, rotating) + fallback partials [2NW, 4NW)
 };
 
 template <int NW>
@@ -381,6 +381,26 @@ __device__ __forceinline__ uint64_t block_min_u64(uint64_t wmin, uint64_t *slots
 #pragma unroll
     for (int q = 1; q < NW; ++q) g = umin64(g, slots[q]);
     return g;
+  }
+}
+
+// Step argmin across the NW waves through one LDS word per step: lane 0 of
+// every wave folds its wave minimum in with ds_min_u64, one barrier, every
+// wave reads the word.  Three words rotate (step t uses word t % 3); thread
+// 0 re-arms word (t + 1) % 3 at the top of step t, in the shadow of the row
+// loads: that word last held step t - 2's minimum, which every wave read
+// before arriving at barrier t - 1, and step t + 1's ds_min ops come after
+// barrier t.  (Built without the atomic optimizer: one lane per wave is
+// already active, the optimizer's lane election would only add VALU.)
+template <int NW>
+__device__ __forceinline__ uint64_t block_min_u64_rot(uint64_t wmin, uint64_t *slots, int s) {
+  if constexpr (NW == 1) {
+    return wmin;
+  } else {
+    if ((threadIdx.x & 63) == 0)
+      __hip_atomic_fetch_min(slots + s, wmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();
+    return slots[s];
   }
 }
 
@@ -409,7 +429,9 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
                         : ((1u << (2 * FB)) | ((uint32_t)pos[k] << FB) | (uint32_t)r4c[k]);
   };
   int64_t steps = 0;
-  int par = 0;
+  int par = 0;  // rotating step-argmin word (0..2)
+  if (NW > 1 && tid < 3) S.red[tid] = ~0ull;
+  __syncthreads();
   for (int cur = 0; cur < n; ++cur) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -428,6 +450,7 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
       const int64_t ui = S.u[i];
       int64_t c[K];
       ld.load(i, c);
+      if (NW > 1 && tid == 0) S.red[par == 2 ? 0 : par + 1] = ~0ull;
       const int64_t kU = minVal - ui;
       const uint64_t kb = (uint64_t)BIAS - (uint64_t)minVal;
       uint64_t best = ~0ull;
@@ -451,10 +474,10 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
         const uint64_t key = ((uint64_t)kh << 32) | ((sl << LOB) | lo[k]);
         best = (act && key < best) ? key : best;
       }
-      uint64_t g = block_min_u64<NW>(wave_min_u64_fast<true>(best), S.red + par * NW, w);
+      uint64_t g = block_min_u64_rot<NW>(wave_min_u64_fast<true>(best), S.red, par);
       g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
-      par ^= 1;
+      par = (par == 2) ? 0 : par + 1;
       const uint64_t hi = g >> LOB;
       if (exact || (uint32_t)(g >> 32) - LOW >= SAT - LOW) {
         // exact two-pass argmin: min spc (signed), then min key-low among ties
