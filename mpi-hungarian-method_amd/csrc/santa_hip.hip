@@ -474,7 +474,19 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
         const uint64_t key = ((uint64_t)kh << 32) | ((sl << LOB) | lo[k]);
         best = (act && key < best) ? key : best;
       }
-      uint64_t g = block_min_u64_rot<NW>(wave_min_u64_fast<true>(best), S.red, par);
+      uint64_t g;
+      if constexpr (NW == 1) {
+        g = wave_min_u64_fast<true>(best);
+      } else {
+        // wave DPP min of the high words; the lanes holding it (usually one)
+        // fold their full keys into the step word
+        const uint32_t bh = (uint32_t)(best >> 32);
+        const uint32_t mh = wave_min_u32_dpp(bh);
+        if (bh == mh && mh != ~0u)
+          __hip_atomic_fetch_min(S.red + par, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __syncthreads();
+        g = S.red[par];
+      }
       g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
       par = (par == 2) ? 0 : par + 1;
