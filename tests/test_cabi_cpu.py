@@ -143,6 +143,25 @@ def test_submission_csv_roundtrip(tmp_path):
     assert np.array_equal(D.read_submission(str(p)), t)
 
 
+def test_v2_csv_readers(tmp_path):
+    """child_wishlist_v2.csv / gift_goodkids_v2.csv: no header, column 0 the
+    id, dropped as mpi_single.py:194,196 do with drop(0, 1)."""
+    sd = D.synthetic(seed=3, nc=20000, ng=20, nq=1000, n_wish=10, n_good=100)
+    wp, gp = tmp_path / "child_wishlist_v2.csv", tmp_path / "gift_goodkids_v2.csv"
+    np.savetxt(wp, np.c_[np.arange(sd.nc), sd.wish], fmt="%d", delimiter=",")
+    np.savetxt(gp, np.c_[np.arange(sd.ng), sd.goodkids], fmt="%d", delimiter=",")
+    w, g = D.read_wishlist(str(wp)), D.read_goodkids(str(gp))
+    assert w.dtype == np.int16 and g.dtype == np.int32
+    assert np.array_equal(w, sd.wish) and np.array_equal(g, sd.goodkids)
+    sub = tmp_path / "baseline_res.csv"
+    D.write_submission(str(sub), sd.types)
+    assert np.array_equal(D.read_submission(str(sub), sd.nc), sd.types)
+    # a child without a gift is an error, not a silent -1
+    open(sub, "w").write("ChildId,GiftId\n0,1\n2,1\n")
+    with pytest.raises(ValueError):
+        D.read_submission(str(sub), 3)
+
+
 def test_hash_cost_host_mirror_shape():
     C = S.hash_matrix(7, 0, 16, 100)
     assert C.shape == (16, 16) and C.min() >= 0 and C.max() < 100
