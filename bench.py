@@ -321,9 +321,13 @@ def main():
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (seeded Kaggle-shaped: 1M children x 100 wishes, 1000 gifts x 1000 good kids)",
-        "config": {"workload": ("singles full round: 3730 disjoint n=256 blocks/round (BASELINE config 2)"
+        "config": {"workload": (f"singles full round: {nb} disjoint n={n} blocks/round"
+                                + (" (BASELINE config 2)" if n == 256 else " (reference block size)"
+                                   if n == 2000 else "")
                                 if mode == 0 else
-                                "twins full round: 78 disjoint 256-pair blocks/round (BASELINE config 3)"),
+                                f"twins full round: {nb} disjoint {n}-pair blocks/round"
+                                + (" (BASELINE config 3)" if n == 256 else " (reference block size)"
+                                   if n == 3000 else "")),
                    "block_n": n, "blocks_per_round": nb, "parallelism": f"blocks sharded over {world} GPU(s)"},
         "score_gain_per_s": gain,
         "score_start": score_start,
