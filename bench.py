@@ -345,14 +345,23 @@ def main():
     # HBM traffic of the same kernel from the committed rocprofv3 PMC passes
     # (tools/profile_round.sh -> profiles/<tag>_summary.json; FETCH_SIZE and
     # WRITE_SIZE in separate passes, KB x 1024, on a full 3730-block round)
+    # FETCH_SIZE is scaled by the factor calibrated for this kernel's access
+    # pattern (random 200-byte wishlist rows, 8-byte lane loads; the guide's
+    # 2x rule holds only for 16 B/lane streams -- tools/calib/gather_calib.hip,
+    # profiles/<tag>_fetch_calibration.json); WRITE_SIZE is taken as read.
     prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))
+    calib = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fetch_calibration.json")))
     if prof and mode == 0 and world == 1:  # the PMC passes profile a full one-GPU round
         try:
             hb = json.load(open(prof[-1]))["hbm_bytes_per_launch"]
             kname = out["roofline"]["kernel"].split(" ")[0].split("<")[0]
             e = hb.get(kname, {})
             if "FETCH_SIZE_bytes" in e and "WRITE_SIZE_bytes" in e:
-                out["roofline"]["traffic"] = e["FETCH_SIZE_bytes"] + e["WRITE_SIZE_bytes"]
+                k = json.load(open(calib[-1]))["gather_correction_factor"] if calib else 1.0
+                out["roofline"]["traffic"] = round(e["FETCH_SIZE_bytes"] * k + e["WRITE_SIZE_bytes"])
+                out["roofline"]["traffic_raw"] = {"FETCH_SIZE": e["FETCH_SIZE_bytes"],
+                                                  "WRITE_SIZE": e["WRITE_SIZE_bytes"],
+                                                  "fetch_correction": round(k, 4)}
                 out["roofline"]["traffic_source"] = os.path.basename(prof[-1])
         except (OSError, KeyError, ValueError):
             pass

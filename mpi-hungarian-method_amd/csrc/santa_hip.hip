@@ -862,14 +862,14 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
       const uint32_t co = tile8[(size_t)i * RS + i];
       cost += single_cost(cn, nw1, a.E);
       dch += child_happy(cn, nw1) - child_happy(co, nw1);
-      dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
+      if (a.delta) dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
     } else {
       const uint16_t *t16 = (const uint16_t *)tile8;
       const uint32_t cn = t16[(size_t)i * RS + col];
       const uint32_t co = t16[(size_t)i * RS + i];
       cost += lut[cn & (TWIN_LUT - 1)];
       dch += twin_lut_happy(cn) - twin_lut_happy(co);
-      dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
+      if (a.delta) dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
              gift_happy(a, child, told) - gift_happy(a, child + 1, told);
     }
   }
@@ -1279,12 +1279,12 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
     if (MODE == 0) {
       cost += single_cost(vn, nw1, a.E);
       dch += child_happy(vn, nw1) - child_happy(vo, nw1);
-      dgh += gift_happy(a, rows_l[rn], tn) - gift_happy(a, rows_l[j], tn);
+      if (a.delta) dgh += gift_happy(a, rows_l[rn], tn) - gift_happy(a, rows_l[j], tn);
     } else {
       cost += twin_cost(vn, nw1, a.E);
       dch += child_happy(vn & 0xFF, nw1) + child_happy(vn >> 8, nw1) -
              child_happy(vo & 0xFF, nw1) - child_happy(vo >> 8, nw1);
-      dgh += gift_happy(a, rows_l[rn], tn) + gift_happy(a, rows_l[rn] + 1, tn) -
+      if (a.delta) dgh += gift_happy(a, rows_l[rn], tn) + gift_happy(a, rows_l[rn] + 1, tn) -
              gift_happy(a, rows_l[j], tn) - gift_happy(a, rows_l[j] + 1, tn);
     }
   }
@@ -1640,7 +1640,7 @@ __global__ __launch_bounds__(WAVE, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
       } else {
         cost += cij;
         dch += child_happy(cn, nw1) - child_happy(co, nw1);
-        dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
+        if (a.delta) dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
       }
       if (a.col) a.col[(size_t)b * n + i] = col;
       a.types[child] = (int16_t)tnew;  // this block owns child; ctype holds old types
@@ -2219,7 +2219,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         const uint32_t cn = (cij == E) ? 0u : (uint32_t)((cij >> 32) + nw1);
         cost += cij;
         dch += child_happy(cn, nw1) - child_happy(co, nw1);
-        dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
+        if (a.delta) dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
       }
       if (a.col) a.col[(size_t)b * n + i] = col;
       a.types[child] = (int16_t)tnew;  // this block owns child; ctype holds old types
@@ -2434,12 +2434,12 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
     if (MODE == 0) {
       cost += single_cost(n1, nw1, a.E);
       dch += child_happy(n1, nw1) - child_happy(o1, nw1);
-      dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
+      if (a.delta) dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
     } else {
       const uint32_t n2 = wish_code(a, child + 1, tnew), o2 = wish_code(a, child + 1, told);
       cost += twin_cost(n1 | (n2 << 8), nw1, a.E);
       dch += child_happy(n1, nw1) + child_happy(n2, nw1) - child_happy(o1, nw1) - child_happy(o2, nw1);
-      dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
+      if (a.delta) dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
              gift_happy(a, child, told) - gift_happy(a, child + 1, told);
     }
     if (a.col) a.col[(size_t)b * n + i] = col;
