@@ -869,7 +869,9 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
       const uint32_t co = t16[(size_t)i * RS + i];
       cost += lut[cn & (TWIN_LUT - 1)];
       dch += twin_lut_happy(cn) - twin_lut_happy(co);
-      if (a.delta) dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
+      // (unconditional: guarding these reads on a.delta, as the other kernels do,
+      // made this kernel 2 % slower in A/B bench runs -- code generation)
+      dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
              gift_happy(a, child, told) - gift_happy(a, child + 1, told);
     }
   }
