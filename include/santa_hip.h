@@ -129,7 +129,7 @@ int sh_sample_blocks(uint64_t seed, uint64_t round, int lo, int count, int strid
  *   d_steps int64 [B]     (nullable)  Dijkstra steps taken per block
  * Returns SH_ERR_ARGS for n > SH_MAX_N_SANTA or rows out of range (checked on the
  * device lazily: an out-of-range block is skipped and reported by
- * sh_ctx_error_flags).
+ * sh_ctx_error_flags).  B = 0 is a no-op (d_rows may then be NULL).
  * ------------------------------------------------------------------------ */
 int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B,
                     int16_t *d_types, int32_t *d_col, int64_t *d_cost,
@@ -191,7 +191,8 @@ int sh_unpack_types(int16_t *d_types, const int32_t *d_rows, int count,
  * f64: bit-exact replay of scipy's float64 arithmetic for ANY finite/+inf
  * input (the caller rejects NaN and -inf, as scipy does).
  * i64: exact for |C| < 2^50 (keeps every dual/distance < 2^62 at n <= 1024);
- * the caller checks the bound (santa_hip.lsap does).
+ * the caller checks the bound (santa_hip.lsap does).  B = 0 is a no-op
+ * (d_C / d_col may then be NULL).
  * ------------------------------------------------------------------------ */
 int lsap_solve_batched_i64(const int64_t *d_C, int n, int B, int32_t *d_col,
                            int64_t *d_cost, unsigned flags, void *stream);

@@ -3039,7 +3039,7 @@ extern "C" {
 int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, int16_t *d_types,
                     int32_t *d_col, int64_t *d_cost, int64_t *d_delta, int64_t *d_steps,
                     unsigned flags, void *stream) {
-  if (!ctx || !d_rows || !d_types) return fail(SH_ERR_ARGS, "null pointer");
+  if (!ctx || (!d_rows && B > 0) || !d_types) return fail(SH_ERR_ARGS, "null pointer");
   if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS) return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA) return fail(SH_ERR_ARGS, "n must be in [1, 4096]");
   if ((int64_t)n * (mode ? 2 : 1) > ctx->nc) return fail(SH_ERR_ARGS, "block larger than the instance");
@@ -3123,7 +3123,7 @@ namespace {
 int check_lsap_args(int n, int B, const int32_t *col) {
   if (n <= 0 || n > SH_MAX_N) return fail(SH_ERR_ARGS, "n must be in [1, 1024]");
   if (B < 0) return fail(SH_ERR_ARGS, "B < 0");
-  if (!col) return fail(SH_ERR_ARGS, "null col");
+  if (!col && B > 0) return fail(SH_ERR_ARGS, "null col");
   return SH_OK;
 }
 
@@ -3168,19 +3168,19 @@ extern "C" {
 
 int lsap_solve_batched_i64(const int64_t *d_C, int n, int B, int32_t *d_col, int64_t *d_cost,
                            unsigned flags, void *stream) {
-  if (!d_C) return fail(SH_ERR_ARGS, "null C");
+  if (!d_C && B > 0) return fail(SH_ERR_ARGS, "null C");
   return launch_lsap_i64<int64_t, false>(d_C, 0, 1, n, B, d_col, d_cost, flags, (hipStream_t)stream);
 }
 
 int lsap_solve_batched_i32(const int32_t *d_C, int n, int B, int32_t *d_col, int64_t *d_cost,
                            unsigned flags, void *stream) {
-  if (!d_C) return fail(SH_ERR_ARGS, "null C");
+  if (!d_C && B > 0) return fail(SH_ERR_ARGS, "null C");
   return launch_lsap_i64<int32_t, false>(d_C, 0, 1, n, B, d_col, d_cost, flags, (hipStream_t)stream);
 }
 
 int lsap_solve_batched_f64(const double *d_C, int n, int B, int32_t *d_col, double *d_cost,
                            unsigned flags, void *stream) {
-  if (!d_C) return fail(SH_ERR_ARGS, "null C");
+  if (!d_C && B > 0) return fail(SH_ERR_ARGS, "null C");
   (void)flags;
   return launch_lsap_f64(d_C, n, B, d_col, d_cost, (hipStream_t)stream);
 }

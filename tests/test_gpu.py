@@ -464,3 +464,55 @@ def test_exchange_over_rccl(sh, ctx, full_data):
             assert torch.equal(types, want), mode
     finally:
         dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------- edge sizes
+@pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 255])
+def test_lsap_edge_sizes_vs_oracle(sh, n):
+    """Wave-boundary and degenerate sizes (one lane, partial waves, one column
+    past a wave) through the batched solver, against the oracle; ties
+    included (small modulus)."""
+    rng = np.random.default_rng(1000 + n)
+    for mod in (3, 1 << 16):
+        C = rng.integers(0, mod, size=(3, n, n), dtype=np.int64)
+        col, cost = sh.solve_batched(torch.from_numpy(C).cuda())
+        ocol, ocost = oracle.lsap_i64_batched(C)
+        assert np.array_equal(col.cpu().numpy(), ocol), (n, mod)
+        assert np.array_equal(cost.cpu().numpy(), ocost), (n, mod)
+
+
+def test_empty_batches_are_noops(sh, ctx, full_data):
+    """B = 0 (an empty shard, e.g. a rank with no blocks) is accepted and
+    changes nothing, like scipy on an empty problem list."""
+    col, cost = sh.solve_batched(torch.empty((0, 8, 8), dtype=torch.int64, device="cuda"))
+    assert col.shape == (0, 8) and cost.shape == (0,)
+    types = ctx.upload_types(full_data.types)
+    ctx.solve_blocks(0, torch.empty(0, dtype=torch.int32, device="cuda"), 256, types)
+    torch.cuda.synchronize()
+    assert np.array_equal(types.cpu().numpy(), full_data.types)
+    assert ctx.error_flags() == 0
+
+
+@pytest.mark.parametrize("mode,n,B", [(0, 1, 5), (0, 2, 7), (0, 63, 3), (0, 65, 3),
+                                      (1, 1, 4), (1, 2, 3), (1, 65, 2)])
+def test_santa_edge_block_sizes_vs_oracle(sh, ctx, full_data, mode, n, B):
+    """Santa blocks of degenerate / wave-boundary sizes: the fused kernels
+    equal the oracle (col, cost, whole type vector, deltas)."""
+    from santa_hip import _lib
+    rows = ctx.sample_blocks(mode, n, B, 77, 2)
+    t_host = full_data.types.copy()
+    ocol, ocost = oracle.round_blocks(mode, full_data.wish, t_host, rows.cpu().numpy().reshape(B, n),
+                                      ng=full_data.ng)
+    s0 = oracle.score_sums(full_data.wish, full_data.goodkids, full_data.types)
+    s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
+    for fl in ((0, _lib.SH_FLAG_SP_TILE) if mode == 0 else (0,)):
+        types = ctx.upload_types(full_data.types)
+        col = torch.empty(B * n, dtype=torch.int32, device="cuda")
+        cost = torch.empty(B, dtype=torch.int64, device="cuda")
+        delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+        ctx.solve_blocks(mode, rows, n, types, col=col, cost=cost, delta=delta, flags=fl)
+        assert np.array_equal(col.cpu().numpy().reshape(B, n), ocol), fl
+        assert np.array_equal(cost.cpu().numpy(), ocost), fl
+        assert np.array_equal(types.cpu().numpy(), t_host), fl
+        assert delta.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]], fl
+        assert ctx.error_flags() == 0
