@@ -8,15 +8,21 @@ vector across ranks (RCCL all-gather, N > 1) and re-score the whole
 assignment (avg_normalized_happiness), reading the score back as the
 reference does every round (mpi_single.py:157-169).
 
-Prints ONE JSON line (rank 0).  value = blocks solved and applied per second,
-whole job; score gain per second is reported beside it.
+`--gpus N` (N > 1) without a torch.distributed environment starts N ranks
+itself (`torch.distributed.run`, a child process; this process touches no
+GPU) and forwards rank 0's line.  Prints ONE JSON line (rank 0).  value =
+blocks solved and applied per second, whole job; score gain per second is
+reported beside it.
 """
 from __future__ import annotations
 
 import argparse
 import glob
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,10 +30,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpi-hungarian-method_amd"))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-LDS_PEAK_GBS = 256 * 128 * 2.4  # 256 CUs x 128 B/clk (ds_read_b32) x 2.4 GHz
+CLOCK_HZ = 2.4e9               # MI355X max shader clock (MI355X_MICROARCH.md)
+KERNEL_SRC = os.path.join(ROOT, "mpi-hungarian-method_amd", "csrc", "santa_hip.hip")
 
 
 def parse():
@@ -39,7 +45,9 @@ def parse():
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--seed", type=int, default=2017)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="budget of the CPU baseline sample (rank 0, N=1 only)")
+                    help="budget of the CPU port / scipy baselines (rank 0, N=1 only)")
+    ap.add_argument("--b1-seconds", type=float, default=6.0,
+                    help="budget per rank count of the reference-semantics baseline B1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl",
                     help="test only: 'gloo' with --one-device rehearses N ranks on one GPU")
@@ -48,7 +56,65 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(sd, mode: int, n: int, seconds: float):
+# --------------------------------------------------------------------------- launcher
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` run by hand: start the N ranks as a child
+    `torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1;
+    the reference's `mpirun -np P`) and exit with its code.  Rank 0's JSON
+    line reaches stdout through the inherited descriptors."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+# --------------------------------------------------------------------------- CPU side
+def cpu_info() -> dict:
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    aff = len(os.sched_getaffinity(0))
+    # the GPU box leases a CPU share per GPU and says so in OMP_NUM_THREADS
+    # (os.cpu_count() there shows the whole machine); otherwise the affinity
+    used = int(omp) if omp and omp.isdigit() and int(omp) > 0 else aff
+    return {"model": model, "nproc": os.cpu_count(), "affinity": aff, "omp_num_threads": omp,
+            "used": min(used, aff)}
+
+
+def b1_baseline(mode: str, n: int, cores: int, seconds: float) -> dict:
+    """B1: the reference's own round loop as written —
+    P ranks, Python n^2 cost loop, scipy, pickled gather/bcast, full rescore
+    and the 1M-row CSV every round (oracle/ref_semantics.py) — at P = 8 and
+    P = all leased cores.  Runs as a child process before this process
+    touches the GPU."""
+    procs = sorted({min(8, cores), cores})
+    cmd = [sys.executable, os.path.join(ROOT, "oracle", "ref_semantics.py"), "--mode", mode,
+           "--n", str(n), "--procs", ",".join(map(str, procs)), "--seconds", str(seconds)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=60 + 4 * seconds * len(procs))
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError) as e:
+        return {"error": f"{type(e).__name__}: {e}"}
+    return {"blocks_per_s": {str(x["procs"]): x["blocks_per_s"] for x in out["runs"]},
+            "score_gain_per_s": {str(x["procs"]): x["score_gain_per_s"] for x in out["runs"]},
+            "rounds": {str(x["procs"]): x["rounds"] for x in out["runs"]},
+            "setup_s": out["setup_s"]}
+
+
+def cpu_baseline(sd, mode: int, n: int, seconds: float, cores: int):
     """The oracle (plain-C port of the reference path: cost build + scipy-exact
     SAP + apply) on the host cores over blocks of the same round: one thread
     per core (ctypes releases the GIL; blocks are disjoint, so the threads
@@ -65,18 +131,13 @@ def cpu_baseline(sd, mode: int, n: int, seconds: float):
         lo, count, nb = twin_geometry(tri, tw, n)
         stride = 2
     rows = sample_blocks(12345, 0, lo, count, stride, n, nb)
-    ncores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1),
-                        len(os.sched_getaffinity(0)), 16))
     t = sd.types.copy()
-    # single core: a few seconds
     done1 = 0
     t0 = time.perf_counter()
     while done1 < nb and time.perf_counter() - t0 < seconds / 4:
         oracle.round_blocks(mode, sd.wish, t, rows[done1:done1 + 8], ng=sd.ng)
         done1 += min(8, nb - done1)
     el1 = time.perf_counter() - t0
-    # all cores: blocks of successive rounds (fresh type vector), chunked over
-    # threads, until the time budget is spent
     t = sd.types.copy()
     deadline = time.perf_counter() + seconds
     doneN = 0
@@ -88,7 +149,7 @@ def cpu_baseline(sd, mode: int, n: int, seconds: float):
         return len(ch)
 
     t1 = time.perf_counter()
-    with cf.ThreadPoolExecutor(ncores) as ex:
+    with cf.ThreadPoolExecutor(cores) as ex:
         rnd = 0
         while time.perf_counter() < deadline:
             rr = rows if rnd == 0 else sample_blocks(12345, rnd, lo, count, stride, n, nb)
@@ -100,18 +161,18 @@ def cpu_baseline(sd, mode: int, n: int, seconds: float):
     oracle.score_sums(sd.wish, sd.goodkids, t)  # the full rescore of each round, 1 core
     score_s = time.perf_counter() - t2
     bpsN = doneN / elN if elN > 0 else 0.0
-    sc_bps, sc_done, sc_el = scipy_baseline(sd, mode, n, min(6.0, seconds / 2), ncores, rows, lo, count,
+    sc_bps, sc_done, sc_el = scipy_baseline(sd, mode, n, min(6.0, seconds / 2), cores, rows, lo, count,
                                             stride, nb)
-    return {"value": round(bpsN, 2), "unit": "blocks/s", "cores": ncores, "kind": "port",
+    return {"value": round(bpsN, 2), "unit": "blocks/s", "cores": cores, "kind": "port",
             "sample": f"{doneN} blocks (n={n}, rounds of {nb}) through oracle.round_blocks "
-                      f"on {ncores} threads in {elN:.1f}s; {done1} blocks on 1 core in {el1:.1f}s; "
+                      f"on {cores} threads in {elN:.1f}s; {done1} blocks on 1 core in {el1:.1f}s; "
                       f"full rescore {score_s:.2f}s per round (1 core)",
             "single_core_blocks_per_s": round(done1 / el1, 2) if el1 > 0 else None,
             "round_blocks_per_s_incl_score": round(nb / (nb / bpsN + score_s), 2) if bpsN > 0 else None,
             "reference_lap_blocks_per_s": round(sc_bps, 2),
             "reference_lap_sample": f"{sc_done} blocks: the reference's float32 happiness values "
                                     f"(mpi_single.py:213-218) gathered per block with numpy + scipy "
-                                    f"linear_sum_assignment (mpi_single.py:101) on {ncores} threads "
+                                    f"linear_sum_assignment (mpi_single.py:101) on {cores} threads "
                                     f"in {sc_el:.1f}s"}
 
 
@@ -157,11 +218,52 @@ def scipy_baseline(sd, mode, n, seconds, ncores, rows, lo, count, stride, nb):
     return (done / el if el > 0 else 0.0), done, el
 
 
+# --------------------------------------------------------------------------- HBM traffic
+def stored_traffic(kname: str):
+    """HBM bytes per launch of `kname` from the newest committed rocprofv3 PMC
+    summary taken on THIS kernel source (tools/profile_round.sh ->
+    profiles/<tag>_summary.json records the source hash).  FETCH_SIZE is
+    scaled by the factor calibrated for this kernel's access pattern (random
+    200-byte wishlist rows, 8-byte lane loads; the guide's 2x rule holds only
+    for 16 B/lane streams: tools/calib/gather_calib.hip,
+    profiles/<tag>_fetch_calibration.json); WRITE_SIZE is taken as read."""
+    src = hashlib.sha256(open(KERNEL_SRC, "rb").read()).hexdigest()[:16]
+    calib = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fetch_calibration.json")))
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
+        try:
+            s = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if s.get("source_sha16") != src:
+            continue
+        e = s.get("hbm_bytes_per_launch", {}).get(kname, {})
+        if "FETCH_SIZE_bytes" in e and "WRITE_SIZE_bytes" in e:
+            k = json.load(open(calib[-1]))["gather_correction_factor"] if calib else 1.0
+            return {"traffic": round(e["FETCH_SIZE_bytes"] * k + e["WRITE_SIZE_bytes"]),
+                    "traffic_raw": {"FETCH_SIZE": e["FETCH_SIZE_bytes"], "WRITE_SIZE": e["WRITE_SIZE_bytes"],
+                                    "fetch_correction": round(k, 4)},
+                    "traffic_source": f"{os.path.basename(path)} (kernel source {src})"}
+    return {"traffic": None,
+            "traffic_note": f"no committed PMC summary was taken on this kernel source ({src})"}
+
+
+# --------------------------------------------------------------------------- main
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
+                 f"--nproc-per-node {args.gpus} or drop WORLD_SIZE")
     local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = cpu_info()
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    # B1 first, in a child process, while nothing here has touched the GPU
+    b1 = b1_baseline(args.mode, args.n, cpu["used"], args.b1_seconds) if want_cpu else None
+
+    import torch
     import santa_hip
     from santa_hip import _lib
     from santa_hip import data as D
@@ -184,12 +286,15 @@ def main():
     types = ctx.upload_types(sd.types)
     backup = torch.empty_like(types)
     _, _, _, nb = ctx.geometry(mode, n)
-    b0, b1, _ = shard_range(nb, rank, world)
+    b0, b1_, _ = shard_range(nb, rank, world)
+    my_blocks = b1_ - b0
     w = World(rank, world, None)
     buffers = {}
     stream = torch.cuda.current_stream(dev)
-    ev = []  # (start, end) events around the fused block kernel, per step
+    ev = []  # (start, end) events around the fused block kernel, per timed step
     state = {"best": None, "score": None}
+    max_rounds = max(args.steps, args.warmup, 1)
+    steps_dev = torch.zeros((max_rounds, max(my_blocks, 1)), dtype=torch.int64, device=dev)
 
     # singles: every round is rescored (as the reference does), but off the
     # critical path -- the score kernel reads a snapshot of the types on a
@@ -199,10 +304,19 @@ def main():
     side = torch.cuda.Stream(dev)
     snaps = [torch.empty_like(types) for _ in range(2)]
     snap_free = [None, None]
-    max_rounds = max(args.steps, args.warmup, 1)
     sums_dev = torch.zeros((max_rounds, 4), dtype=torch.int64, device=dev)
     sums_host = torch.zeros((max_rounds, 4), dtype=torch.int64).pin_memory()
     pending = []
+
+    class _Eng:
+        def __init__(self, c):
+            self.c = c
+
+        def pack_types(self, t, r, o):
+            self.c.pack_types(t, r, o)
+
+        def unpack_types(self, t, r, v, m):
+            self.c.unpack_types(t, r, v, m)
 
     def step(rnd: int, timed: bool):
         rows = ctx.sample_blocks(mode, n, nb, args.seed, rnd)
@@ -212,8 +326,10 @@ def main():
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        if b1 > b0:
-            ctx.solve_blocks(mode, rows[b0 * n:b1 * n], n, types)
+        if my_blocks:
+            # steps per block of the timed launches feed the latency view below
+            ctx.solve_blocks(mode, rows[b0 * n:b1_ * n], n, types,
+                             steps=steps_dev[rnd] if timed else None)
         if timed:
             e1.record(stream)
             ev.append((e0, e1))
@@ -252,16 +368,6 @@ def main():
             state["score"] = s
         pending.clear()
 
-    class _Eng:
-        def __init__(self, c):
-            self.c = c
-
-        def pack_types(self, t, r, o):
-            self.c.pack_types(t, r, o)
-
-        def unpack_types(self, t, r, v, m):
-            self.c.unpack_types(t, r, v, m)
-
     sc0, sg0, _, _ = ctx.score_sums(types)
     score0 = santa_hip.score_from_sums(sc0, sg0, ctx.nc, ctx.ng, ctx.n_wish, ctx.n_good)
     # warm up on the same rounds, then restart from the baseline assignment so
@@ -297,17 +403,53 @@ def main():
     blocks_total = nb * args.steps
     value = blocks_total / elapsed
     gain = (state["best"] - score_start) / elapsed
-    # roofline of the dominant kernel (fused cost build + SAP + apply)
+
+    # -- roofline of the dominant kernel (fused cost build + SAP + apply) ------
+    design = ctx.solve_design(mode, n, max(my_blocks, 1))
+    kname = _lib.SH_DESIGN_NAMES[design]
     per_block = (208 if mode == 0 else 408) * n  # algorithmic HBM bytes / block
-    my_blocks = b1 - b0
     achieved = per_block * my_blocks / kern_avg_s / 1e9 if kern_avg_s > 0 else 0.0
-    # step statistics for the LDS/latency view (one extra, untimed launch)
-    steps_t = torch.empty(max(my_blocks, 1), dtype=torch.int64, device=dev)
-    rows = ctx.sample_blocks(mode, n, nb, args.seed, 10_000)
-    tmp = types.clone()
-    ctx.solve_blocks(mode, rows[b0 * n:b1 * n], n, tmp, steps=steps_t)
-    dsteps = int(steps_t[:my_blocks].sum().item())
-    lds_bytes = dsteps * (n + 8)  # one tile row + u[i] per Dijkstra step
+    # latency / occupancy view from the Dijkstra steps of the TIMED launches:
+    # the kernel is a serial chain of Dijkstra steps per block.  The lone
+    # per-step latency is measured by re-running round 0's longest block
+    # alone (same kernel design, untimed region).
+    latency = None
+    if my_blocks:
+        st = steps_dev[:args.steps, :my_blocks].cpu().numpy().astype(np.int64)
+        bmax = int(st[0].argmax())
+        rows0 = ctx.sample_blocks(mode, n, nb, args.seed, 0)
+        one = rows0[(b0 + bmax) * n:(b0 + bmax + 1) * n].contiguous()
+        force = {0: _lib.SH_FLAG_SP_TILE, 1: _lib.SH_FLAG_LDS_TILE}.get(design, 0)
+        lone = []
+        for _ in range(3):
+            tt = ctx.upload_types(sd.types)
+            s1 = torch.zeros(1, dtype=torch.int64, device=dev)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            ctx.solve_blocks(mode, one, n, tt, steps=s1, flags=force)
+            b.record(stream)
+            torch.cuda.synchronize()
+            lone.append(a.elapsed_time(b) / 1e3)
+        lone_steps = int(s1.item())
+        s_per_step = min(lone) / max(lone_steps, 1)
+        resident = ctx.resident_blocks(mode, n, my_blocks)
+        chain_floor = float(st.max(axis=1).sum()) * s_per_step          # longest block per round
+        occ_floor = float(st.sum()) * s_per_step / max(min(resident, my_blocks), 1)
+        kern_sum = float(np.sum(kern_ms)) / 1e3
+        floor = max(chain_floor, occ_floor)
+        latency = {"steps_per_launch": float(st.sum(axis=1).mean()),
+                   "steps_max_block_per_launch": float(st.max(axis=1).mean()),
+                   "round0_steps": int(st[0].sum()), "round0_max_block_steps": int(st[0].max()),
+                   "lone_block_steps": lone_steps, "lone_block_ms": round(min(lone) * 1e3, 4),
+                   "cycles_per_step_lone": round(s_per_step * CLOCK_HZ, 1),
+                   "resident_blocks": resident,
+                   "chain_floor_ms_per_launch": round(chain_floor / args.steps * 1e3, 4),
+                   "occupancy_floor_ms_per_launch": round(occ_floor / args.steps * 1e3, 4),
+                   "binding": "longest block's Dijkstra chain" if chain_floor >= occ_floor else
+                              "resident blocks x per-step latency",
+                   "frac": round(floor / kern_sum, 4) if kern_sum > 0 else None,
+                   "note": "floors are lower bounds on the launch time from the lone per-step latency "
+                           "(no co-resident wave contention); frac = floor / measured kernel time"}
     out = {
         "metric": "assignment blocks solved/sec (n=256) + score gain/sec at 1/2/4/8 GPUs",
         "value": round(value, 2),
@@ -328,50 +470,45 @@ def main():
                                 f"twins full round: {nb} disjoint {n}-pair blocks/round"
                                 + (" (BASELINE config 3)" if n == 256 else " (reference block size)"
                                    if n == 3000 else "")),
-                   "block_n": n, "blocks_per_round": nb, "parallelism": f"blocks sharded over {world} GPU(s)"},
+                   "block_n": n, "blocks_per_round": nb,
+                   "parallelism": f"blocks sharded over {world} rank(s)"
+                                  + (" on one device (test)" if args.one_device and world > 1 else
+                                     " = GPU(s)")},
         "score_gain_per_s": gain,
         "score_start": score_start,
         "score_end": state["best"],
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "latency", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": _lib.SH_DESIGN_NAMES[ctx.solve_design(mode, n, max(my_blocks, 1))],
-                     "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
-                     "algorithmic_bytes_per_block": per_block,
-                     "lds": {"bytes_per_launch": lds_bytes,
-                             "achieved_GBs": round(lds_bytes / kern_avg_s / 1e9, 2),
-                             "peak_GBs": LDS_PEAK_GBS},
-                     "dijkstra_steps_per_launch": dsteps},
+                     "hbm_note": "achieved/peak/frac/traffic are the HBM view (algorithmic bytes "
+                                 "per block / kernel time); the kernel is bound by its serial "
+                                 "Dijkstra chains, see latency",
+                     "kernel": kname, "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
+                     "algorithmic_bytes_per_block": per_block, "latency": latency},
+        "cpu": cpu,
     }
-    # HBM traffic of the same kernel from the committed rocprofv3 PMC passes
-    # (tools/profile_round.sh -> profiles/<tag>_summary.json; FETCH_SIZE and
-    # WRITE_SIZE in separate passes, KB x 1024, on a full 3730-block round)
-    # FETCH_SIZE is scaled by the factor calibrated for this kernel's access
-    # pattern (random 200-byte wishlist rows, 8-byte lane loads; the guide's
-    # 2x rule holds only for 16 B/lane streams -- tools/calib/gather_calib.hip,
-    # profiles/<tag>_fetch_calibration.json); WRITE_SIZE is taken as read.
-    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))
-    calib = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fetch_calibration.json")))
-    if prof and mode == 0 and world == 1:  # the PMC passes profile a full one-GPU round
-        try:
-            hb = json.load(open(prof[-1]))["hbm_bytes_per_launch"]
-            kname = out["roofline"]["kernel"].split(" ")[0].split("<")[0]
-            e = hb.get(kname, {})
-            if "FETCH_SIZE_bytes" in e and "WRITE_SIZE_bytes" in e:
-                k = json.load(open(calib[-1]))["gather_correction_factor"] if calib else 1.0
-                out["roofline"]["traffic"] = round(e["FETCH_SIZE_bytes"] * k + e["WRITE_SIZE_bytes"])
-                out["roofline"]["traffic_raw"] = {"FETCH_SIZE": e["FETCH_SIZE_bytes"],
-                                                  "WRITE_SIZE": e["WRITE_SIZE_bytes"],
-                                                  "fetch_correction": round(k, 4)}
-                out["roofline"]["traffic_source"] = os.path.basename(prof[-1])
-        except (OSError, KeyError, ValueError):
-            pass
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(sd, mode, n, args.cpu_seconds)
+    if mode == 0 and world == 1:  # the PMC passes profile a full one-GPU round
+        out["roofline"].update(stored_traffic(kname.split(" ")[0].split("<")[0]))
+    if want_cpu:
+        cb = cpu_baseline(sd, mode, n, args.cpu_seconds, cpu["used"])
+        cb["cpu_model"] = cpu["model"]
+        cb["nproc"] = cpu["nproc"]
+        if b1 is not None and "blocks_per_s" in b1:
+            cb["b1_blocks_per_s"] = b1["blocks_per_s"]
+            cb["b1_score_gain_per_s"] = b1["score_gain_per_s"]
+            cb["b1_sample"] = (f"oracle/ref_semantics.py: the reference's round as written "
+                               f"(mpi_single.py:119-181) with P ranks = {list(b1['blocks_per_s'])} "
+                               f"worker processes, {b1['rounds']} rounds in {args.b1_seconds}s each: "
+                               f"P blocks per round, Python n^2 cost loop, scipy, pickled "
+                               f"gather/bcast, full rescore and the 1M-row CSV per round")
+        elif b1 is not None:
+            cb["b1_error"] = b1.get("error")
+        out["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -144,6 +144,11 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B,
  * Identical results either way.                                            */
 int sh_solve_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags);
 
+/* How many blocks of that design the device runs at once (occupancy of the
+ * kernel x compute units), or < 0 on bad arguments.  A launch of more blocks
+ * runs them in successive dispatch waves (benchmark/roofline bookkeeping).  */
+int sh_resident_blocks(sh_ctx *ctx, int mode, int n, int B, unsigned flags);
+
 /* ---------------------------------------------------------------------------
  * Score sums.  Replaces avg_normalized_happiness (mpi_single.py:13-83):
  *   d_sums int64 [4] = (S_child, S_gift, bad_triplets, bad_twins)
@@ -153,8 +158,12 @@ int sh_solve_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags);
  * ------------------------------------------------------------------------ */
 int sh_score(sh_ctx *ctx, const int16_t *d_types, int64_t *d_sums, void *stream);
 
-/* Device-side error flags of the context (bit 0: a block had rows out of
- * range; bit 1: infeasible solve).  Synchronises `stream`; clears the flags. */
+/* Device-side error flags of the context, or-ed over the calls since the
+ * last read.  A flagged block is skipped whole (its children keep their
+ * types).  Synchronises `stream`; clears the flags.                        */
+#define SH_ERRF_ROWS 1u       /* a block had child ids out of [0, nc)        */
+#define SH_ERRF_INFEASIBLE 2u /* infeasible solve                            */
+#define SH_ERRF_TYPE 4u       /* a block's current gift type outside [0, ng) */
 int sh_ctx_error_flags(sh_ctx *ctx, void *stream);
 
 /* Tuning / test hook of the default singles kernel: LDS bytes per block

@@ -746,7 +746,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
     rows_l[j] = r;
   }
   if (__syncthreads_or(bad)) {
-    if (tid == 0) atomicOr(a.err, 1);
+    if (tid == 0) atomicOr(a.err, SH_ERRF_ROWS);
     return;
   }
   for (int t = tid; t < a.ng; t += SANTA_WG) head[t] = -1;
@@ -755,13 +755,19 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
     const int n16 = (int)((size_t)n * RS * (MODE ? 2 : 1) / 16);
     for (int q = tid; q < n16; q += SANTA_WG) t4[q] = make_uint4(0, 0, 0, 0);
   }
-  __syncthreads();
-  // -- column gift types and type -> column chains ------------------------
+  // -- column gift types (range-checked: they index LDS tables) -----------
+  int badt = 0;
   for (int j = tid; j < n; j += SANTA_WG) {
     const int16_t ty = a.types[rows_l[j]];
-    nxt[j] = (int16_t)atomicExch(&head[ty], j);
+    badt |= (ty < 0) || (ty >= a.ng);
     ctype[j] = ty;
   }
+  if (__syncthreads_or(badt)) {
+    if (tid == 0) atomicOr(a.err, SH_ERRF_TYPE);
+    return;
+  }
+  // -- type -> column chains ------------------------------------------------
+  for (int j = tid; j < n; j += SANTA_WG) nxt[j] = (int16_t)atomicExch(&head[ctype[j]], j);
   __syncthreads();
   // -- fill wish ranks ------------------------------------------------------
   // Virtual rows = the block's children (twins: both twins of each pair).
@@ -1052,15 +1058,18 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
     rows_l[tid] = r;
   }
   if (__syncthreads_or(bad)) {
-    if (tid == 0) atomicOr(a.err, 1);
+    if (tid == 0) atomicOr(a.err, SH_ERRF_ROWS);
     return;
   }
   for (int t = tid; t < a.ng; t += VT_WG) head[t] = -1;
-  __syncthreads();
   const int j = tid;  // this thread's column
   int16_t my_type = -1;
+  if (j < n) my_type = a.types[rows_l[j]];
+  if (__syncthreads_or(j < n && (my_type < 0 || my_type >= a.ng))) {  // types index LDS tables
+    if (tid == 0) atomicOr(a.err, SH_ERRF_TYPE);
+    return;
+  }
   if (j < n) {
-    my_type = a.types[rows_l[j]];
     nxt[j] = (int16_t)atomicExch(&head[my_type], j);
     ctype[j] = my_type;
     c4r_l[j] = -1;
@@ -1405,16 +1414,22 @@ __global__ __launch_bounds__(WAVE, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
     rows_l[j] = r;
   }
   if (__any(bad)) {
-    if (lane == 0) atomicOr(a.err, 1);
+    if (lane == 0) atomicOr(a.err, SH_ERRF_ROWS);
     return;
   }
   for (int t = lane; t < a.ng; t += WAVE) head[t] = -1;
-  __syncthreads();
+  int badt = 0;
   for (int j = lane; j < n; j += WAVE) {
     const int16_t ty = a.types[rows_l[j]];
+    badt |= (ty < 0) || (ty >= a.ng);
     ctype[j] = ty;
-    nxt[j] = (int16_t)atomicExch(&head[ty], j);
   }
+  if (__any(badt)) {  // types index LDS tables
+    if (lane == 0) atomicOr(a.err, SH_ERRF_TYPE);
+    return;
+  }
+  __syncthreads();
+  for (int j = lane; j < n; j += WAVE) nxt[j] = (int16_t)atomicExch(&head[ctype[j]], j);
   __syncthreads();
 
   // -- build: rows 0..127 staged in the LDS tile area and moved to VGPRs, then
@@ -1778,7 +1793,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     bad |= (r < n) && ((child[k] < 0) || (child[k] >= a.nc));
   }
   if (__any(bad)) {
-    if (lane == 0) atomicOr(a.err, 1);
+    if (lane == 0) atomicOr(a.err, SH_ERRF_ROWS);
     return;
   }
   // Warm the TLB and L2 with the block's 256 wishlist rows (random children,
@@ -1800,6 +1815,15 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
   int myt[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) myt[k] = (4 * lane + k < n) ? a.types[child[k]] : -1;
+  {  // the types index LDS tables: reject the block if one is out of range
+    int badt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) badt |= (4 * lane + k < n) && (myt[k] < 0 || myt[k] >= a.ng);
+    if (__any(badt)) {
+      if (lane == 0) atomicOr(a.err, SH_ERRF_TYPE);
+      return;
+    }
+  }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -2180,9 +2204,10 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)c4r, pl);
         const int t = (int)((cw >> ps) & 0xFFu);
         const uint32_t nw4 = (cw & ~(0xFFu << ps)) | ((uint32_t)j << ps);
-        // (lane select through M0: one SGPR operand per VOP3 on gfx950; nothing
-        // else in this kernel keeps a value in M0 -- checked in the ISA)
-        asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(c4r) : "s"(nw4), "s"(pl));
+        // (v_writelane with the lane select in M0: one SGPR operand per VOP3 on
+        // gfx950; the "{m0}" constraint makes the compiler load M0 itself, so it
+        // knows the register is written here)
+        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(c4r) : "s"(nw4), "{m0}"(pl));
 #pragma unroll
         for (int k = 0; k < 4; ++k) r4c[k] = (4 * lane + k == j) ? pi : r4c[k];
         j = t;
@@ -2375,7 +2400,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
     rows_l[j] = r;
   }
   if (__syncthreads_or(bad)) {
-    if (tid == 0) atomicOr(a.err, 1);
+    if (tid == 0) atomicOr(a.err, SH_ERRF_ROWS);
     return;
   }
   for (int t = tid; t < a.ng; t += WG) thead[t] = 0u;
@@ -2387,11 +2412,17 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
   }
   __syncthreads();
   // -- columns sorted by gift type (counting sort) ----------------------------------
+  int badt = 0;
   for (int j = tid; j < n; j += WG) {
     const int ty = a.types[rows_l[j]];
+    badt |= (ty < 0) || (ty >= a.ng);
     ctype[j] = (int16_t)ty;
-    atomicAdd(&thead[ty], 1u << 16);
   }
+  if (__syncthreads_or(badt)) {  // the types index LDS tables
+    if (tid == 0) atomicOr(a.err, SH_ERRF_TYPE);
+    return;
+  }
+  for (int j = tid; j < n; j += WG) atomicAdd(&thead[ctype[j]], 1u << 16);
   __syncthreads();
   {  // block-wide exclusive scan of the counts over types
     const int per = (a.ng + WG - 1) / WG;
@@ -2727,6 +2758,32 @@ int64_t miss_units(int n_wish) {
   return (int64_t)((double)e * 2147483648.0);
 }
 
+// Makes `device` current for the lifetime of the guard and restores the
+// caller's device afterwards: every context entry point runs on the context's
+// device (allocations, kernel attributes, launches) whatever is current.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != device) (void)hipSetDevice(device);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// Dynamic-LDS attribute already raised for a kernel, per device (attributes
+// are per device; a process may drive several).
+constexpr int MAX_DEVICES = 64;
+struct AttrCache {
+  size_t bytes[MAX_DEVICES] = {};
+  bool need(int dev, size_t want) const { return dev < 0 || dev >= MAX_DEVICES || bytes[dev] < want; }
+  void set(int dev, size_t b) {
+    if (dev >= 0 && dev < MAX_DEVICES) bytes[dev] = b;
+  }
+};
+
 }  // namespace
 
 struct sh_ctx {
@@ -2830,6 +2887,7 @@ int sh_ctx_create(sh_ctx **out, int device, const int16_t *h_wish, int n_wish,
         return fail(SH_ERR_ARGS, "twin cost decode mismatch");
     }
   }
+  DeviceGuard dg(device);  // the caller's device is current again on return
   sh_ctx *ctx = new sh_ctx();
   ctx->device = device;
   ctx->nc = nc; ctx->ng = ng; ctx->nq = nq; ctx->n_wish = n_wish; ctx->n_good = n_good;
@@ -2860,6 +2918,7 @@ int sh_ctx_create(sh_ctx **out, int device, const int16_t *h_wish, int n_wish,
 
 void sh_ctx_destroy(sh_ctx *ctx) {
   if (!ctx) return;
+  DeviceGuard dg(ctx->device);
   if (ctx->d_wish) (void)hipFree(ctx->d_wish);
   if (ctx->d_csr_off) (void)hipFree(ctx->d_csr_off);
   if (ctx->d_csr) (void)hipFree(ctx->d_csr);
@@ -2877,6 +2936,7 @@ int sh_ctx_set_sparse_budget(sh_ctx *ctx, int bytes) {
 
 int sh_ctx_error_flags(sh_ctx *ctx, void *stream) {
   if (!ctx) return fail(SH_ERR_ARGS, "null ctx");
+  DeviceGuard dg(ctx->device);
   int32_t h = 0;
   HIP_TRY(hipMemcpyAsync(&h, ctx->d_err, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -2905,11 +2965,11 @@ template <int K, int MODE>
 int launch_santa(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   const SantaLds L = santa_lds_layout(a.n, MODE, ctx->ng);
   if (L.total > 160 * 1024) return fail(SH_ERR_ARGS, "block too large for the LDS tile");
-  static thread_local size_t attr_set = 0;
-  if (L.total > 64 * 1024 && L.total > attr_set) {
+  static thread_local AttrCache attr;
+  if (L.total > 64 * 1024 && attr.need(ctx->device, L.total)) {
     HIP_TRY(hipFuncSetAttribute((const void *)santa_block_kernel<K, MODE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total));
-    attr_set = L.total;
+    attr.set(ctx->device, L.total);
   }
   hipLaunchKernelGGL((santa_block_kernel<K, MODE>), dim3(B), dim3(SANTA_WG), L.total, s, a);
   HIP_TRY(hipGetLastError());
@@ -2936,11 +2996,11 @@ template <int MODE, int NW, int K, int FB>
 int launch_big_cfg(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   const BigLds L = big_lds_layout(a.n, MODE, ctx->ng, NW);
   if (L.total > 160 * 1024) return fail(SH_ERR_ARGS, "block too large for LDS");
-  static thread_local size_t attr_set = 0;
-  if (L.total > 64 * 1024 && L.total > attr_set) {
+  static thread_local AttrCache attr;
+  if (L.total > 64 * 1024 && attr.need(ctx->device, L.total)) {
     HIP_TRY(hipFuncSetAttribute((const void *)santa_big_kernel<MODE, NW, K, FB>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total));
-    attr_set = L.total;
+    attr.set(ctx->device, L.total);
   }
   hipLaunchKernelGGL((santa_big_kernel<MODE, NW, K, FB>), dim3(B), dim3(NW * WAVE), L.total, s, a);
   HIP_TRY(hipGetLastError());
@@ -2989,7 +3049,12 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   f.bcount = a.ovf_cnt;
   f.ovf_reset = ctx->d_ovf + (p ^ 1);
   const int rc = launch_santa_vt<0>(ctx, f, B, s);
-  if (rc) return rc;
+  if (rc) {
+    // the sparse launch may have appended to counter p: clear it so that a
+    // later call's fallback never walks these stale block ids
+    (void)hipMemsetAsync(ctx->d_ovf + p, 0, sizeof(int32_t), s);
+    return rc;
+  }
   ctx->ovf_par = p ^ 1;
   return SH_OK;
 }
@@ -3032,6 +3097,42 @@ int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   if (B <= lds_tile_slots(ctx, n)) return SH_DESIGN_LDS_TILE;
   return SH_DESIGN_SPARSE;
 }
+
+// Blocks of kernel f the device holds at once (occupancy API x CUs).
+template <typename F>
+int occ_blocks(const sh_ctx *ctx, F f, int threads, size_t lds) {
+  if (lds > 160 * 1024) return 0;
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, threads, lds) != hipSuccess) return 0;
+  return per_cu * ctx->n_cu;
+}
+
+template <int MODE>
+int big_resident(const sh_ctx *ctx, int n) {  // mirrors launch_santa_big's configurations
+#define BR_(NW, K, FB) \
+  return occ_blocks(ctx, santa_big_kernel<MODE, NW, K, FB>, NW * WAVE, big_lds_layout(n, MODE, ctx->ng, NW).total)
+  if (n <= 512) BR_(8, 1, 10);
+  if (n <= 1024) BR_(16, 1, 10);
+  if (n <= 2048) BR_(16, 2, 12);
+  if (n <= 3072) BR_(16, 3, 12);
+  BR_(16, 4, 12);
+#undef BR_
+}
+
+int resident_blocks(sh_ctx *ctx, int design, int mode, int n) {
+  switch (design) {
+    case SH_DESIGN_LARGE: return mode == SH_MODE_SINGLE ? big_resident<0>(ctx, n) : big_resident<1>(ctx, n);
+    case SH_DESIGN_TWINS:
+      return occ_blocks(ctx, santa_block_kernel<1, 1>, SANTA_WG, santa_lds_layout(n, 1, ctx->ng).total);
+    case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
+    case SH_DESIGN_SW_TILE: return occ_blocks(ctx, santa_sw_kernel, WAVE, sw_lds_layout(ctx->ng).total);
+    case SH_DESIGN_VT_TILE: return occ_blocks(ctx, santa_vt_kernel<0>, VT_WG, vt_lds_layout(ctx->ng).total);
+    default:
+      return occ_blocks(ctx, santa_sp_kernel<true>, WAVE, sp_lds_layout(ctx->ng, sp_capacity(ctx)).total);
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -3045,6 +3146,7 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   if ((int64_t)n * (mode ? 2 : 1) > ctx->nc) return fail(SH_ERR_ARGS, "block larger than the instance");
   if (B < 0) return fail(SH_ERR_ARGS, "B < 0");
   if (B == 0) return SH_OK;
+  DeviceGuard dg(ctx->device);
   SantaArgs a;
   a.rows = d_rows; a.types = d_types; a.col = d_col; a.cost = d_cost; a.delta = d_delta;
   a.steps = d_steps; a.wish = ctx->d_wish; a.csr_off = ctx->d_csr_off; a.csr = ctx->d_csr;
@@ -3068,11 +3170,21 @@ int sh_solve_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   if (!ctx) return fail(SH_ERR_ARGS, "null ctx");
   if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS) return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA || B < 0) return fail(SH_ERR_ARGS, "bad n or B");
+  DeviceGuard dg(ctx->device);
   return pick_design(ctx, mode, n, B, flags);
+}
+
+int sh_resident_blocks(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
+  if (!ctx) return fail(SH_ERR_ARGS, "null ctx");
+  if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS) return fail(SH_ERR_ARGS, "bad mode");
+  if (n <= 0 || n > SH_MAX_N_SANTA || B < 0) return fail(SH_ERR_ARGS, "bad n or B");
+  DeviceGuard dg(ctx->device);
+  return resident_blocks(ctx, pick_design(ctx, mode, n, B, flags), mode, n);
 }
 
 int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream) {
   if (!ctx) return fail(SH_ERR_ARGS, "null ctx");
+  DeviceGuard dg(ctx->device);
   int32_t h = 0;
   HIP_TRY(hipMemcpyAsync(&h, ctx->d_err + 1, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -3082,6 +3194,7 @@ int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream) {
 
 int sh_score(sh_ctx *ctx, const int16_t *d_types, int64_t *d_sums, void *stream) {
   if (!ctx || !d_types || !d_sums) return fail(SH_ERR_ARGS, "null pointer");
+  DeviceGuard dg(ctx->device);
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipMemsetAsync(d_sums, 0, 4 * sizeof(int64_t), s));
   ScoreArgs a;

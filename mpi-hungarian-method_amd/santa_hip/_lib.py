@@ -26,6 +26,9 @@ SH_FLAG_SW_TILE = 16
 SH_FLAG_VT_TILE = 32
 SH_FLAG_TIMING = 64
 SH_FLAG_SP_TILE = 128
+SH_ERRF_ROWS = 1
+SH_ERRF_INFEASIBLE = 2
+SH_ERRF_TYPE = 4
 SH_DESIGN_NAMES = {0: "santa_sp_kernel (1-wave sparse LDS tile)", 1: "santa_block_kernel (4-wave LDS byte tile)",
                    2: "santa_sw_kernel (1-wave register tile)", 3: "santa_vt_kernel (4-wave register tile)",
                    4: "santa_block_kernel (twins, 4-wave code-pair tile)",
@@ -51,6 +54,7 @@ SIGNATURES = {
     "sh_ctx_error_flags": (_I, [_P, _P]),
     "sh_ctx_fallback_steps": (_I, [_P, _P]),
     "sh_solve_design": (_I, [_P, _I, _I, _I, _U]),
+    "sh_resident_blocks": (_I, [_P, _I, _I, _I, _U]),
     "sh_ctx_set_sparse_budget": (_I, [_P, _I]),
     "sh_pack_types": (_I, [_P, _P, _I, _P, _P]),
     "sh_unpack_types": (_I, [_P, _P, _I, _P, _I, _P]),

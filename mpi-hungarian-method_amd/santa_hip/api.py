@@ -44,7 +44,7 @@ def session() -> SantaGPU:
 
 def _types_from_pred(pred: np.ndarray, nc: int) -> np.ndarray:
     pred = np.asarray(pred)
-    types = np.full(nc, -1, dtype=np.int16)
+    types = np.full(nc, -1, dtype=np.int64)  # int64: out-of-range gifts raise, not wrap
     types[pred[:, 0].astype(np.int64)] = pred[:, 1]
     if (types < 0).any():
         raise ValueError("pred must assign a gift to every child")
@@ -99,7 +99,7 @@ def optimize_block(child_block, current_gift_ids):
     child_block = np.asarray(child_block)
     current_gift_ids = np.asarray(current_gift_ids)
     gift_block = current_gift_ids[child_block]
-    types = (current_gift_ids // s.nq).astype(np.int16)
+    types = current_gift_ids.astype(np.int64) // s.nq  # range-checked by upload_types
     col = _solve_one(_lib.SH_MODE_SINGLE, child_block, types)
     return child_block, gift_block[col]
 
@@ -111,5 +111,5 @@ def optimize_block_twins(child_block, subm):
     child_block = np.asarray(child_block).astype(np.int64)
     gifts = subm["GiftId"].to_numpy() if hasattr(subm, "columns") else np.asarray(subm)
     gift_block = gifts[child_block]
-    col = _solve_one(_lib.SH_MODE_TWINS, child_block, gifts.astype(np.int16))
+    col = _solve_one(_lib.SH_MODE_TWINS, child_block, gifts.astype(np.int64))
     return child_block, gift_block[col]

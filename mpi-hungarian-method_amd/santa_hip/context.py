@@ -75,6 +75,13 @@ class SantaGPU:
 
     # -- state ----------------------------------------------------------------
     def upload_types(self, types: np.ndarray) -> torch.Tensor:
+        """Gift type per child -> device int16 [nc].  Every type must be in
+        [0, ng): the kernels index on-chip tables with it (the reference's
+        numpy indexing raises IndexError on such input)."""
+        types = np.asarray(types)
+        if types.shape != (self.nc,):
+            raise ValueError(f"expected {self.nc} gift types, got shape {types.shape}")
+        check_types(types, self.ng)
         t = torch.from_numpy(np.ascontiguousarray(types, dtype=np.int16))
         return t.to(self.device)
 
@@ -97,8 +104,9 @@ class SantaGPU:
         if B > nb:
             raise ValueError(f"only {nb} disjoint blocks of {n} exist, asked for {B}")
         rows = out if out is not None else torch.empty(B * n, dtype=torch.int32, device=self.device)
-        rc = _lib.lib().sh_sample_blocks(ctypes.c_uint64(seed), ctypes.c_uint64(round_), lo, count,
-                                         stride, n, B, _ptr(rows), self.stream)
+        with torch.cuda.device(self.device):  # (no context: launches on the current device)
+            rc = _lib.lib().sh_sample_blocks(ctypes.c_uint64(seed), ctypes.c_uint64(round_), lo,
+                                             count, stride, n, B, _ptr(rows), self.stream)
         _lib.check(rc, "sh_sample_blocks")
         return rows
 
@@ -125,6 +133,11 @@ class SantaGPU:
         """The kernel design (SH_DESIGN_*) solve_blocks dispatches to."""
         rc = _lib.lib().sh_solve_design(self._h, mode, n, B, _lib.SH_COMPAT_TIEBREAK | flags)
         return _lib.check(rc, "sh_solve_design")
+
+    def resident_blocks(self, mode: int, n: int, B: int, flags: int = 0) -> int:
+        """Blocks of that launch's kernel the device runs at once."""
+        rc = _lib.lib().sh_resident_blocks(self._h, mode, n, B, _lib.SH_COMPAT_TIEBREAK | flags)
+        return _lib.check(rc, "sh_resident_blocks")
 
     def error_flags(self) -> int:
         return _lib.check(_lib.lib().sh_ctx_error_flags(self._h, self.stream), "sh_ctx_error_flags")
@@ -161,14 +174,26 @@ class SantaGPU:
 
     # -- exchange helpers (multi-GPU) ---------------------------------------------
     def pack_types(self, types: torch.Tensor, rows: torch.Tensor, out: torch.Tensor) -> None:
-        rc = _lib.lib().sh_pack_types(_ptr(types), _ptr(rows), rows.numel(), _ptr(out), self.stream)
+        with torch.cuda.device(self.device):
+            rc = _lib.lib().sh_pack_types(_ptr(types), _ptr(rows), rows.numel(), _ptr(out),
+                                          self.stream)
         _lib.check(rc, "sh_pack_types")
 
     def unpack_types(self, types: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor,
                      mode: int) -> None:
-        rc = _lib.lib().sh_unpack_types(_ptr(types), _ptr(rows), rows.numel(), _ptr(vals), mode,
-                                        self.stream)
+        with torch.cuda.device(self.device):
+            rc = _lib.lib().sh_unpack_types(_ptr(types), _ptr(rows), rows.numel(), _ptr(vals), mode,
+                                            self.stream)
         _lib.check(rc, "sh_unpack_types")
+
+
+def check_types(types: np.ndarray, ng: int) -> None:
+    """Reject gift types outside [0, ng) (a missing child is -1)."""
+    if types.size:
+        lo, hi = int(types.min()), int(types.max())
+        if lo < 0 or hi >= ng:
+            bad = int(np.flatnonzero((types < 0) | (types >= ng))[0])
+            raise ValueError(f"gift type {int(types[bad])} of child {bad} is outside [0, {ng})")
 
 
 def score_from_sums(s_child: int, s_gift: int, nc: int, ng: int, n_wish: int, n_good: int) -> float:

@@ -75,13 +75,20 @@ def read_goodkids(path: str) -> np.ndarray:
     return pd.read_csv(path, header=None).drop(columns=0).values.astype(np.int32)
 
 
-def read_submission(path: str, nc: int | None = None) -> np.ndarray:
-    """baseline_res.csv / improved_sub.csv -> int16 gift type per ChildId."""
+def read_submission(path: str, nc: int | None = None, ng: int | None = None) -> np.ndarray:
+    """baseline_res.csv / improved_sub.csv -> int16 gift type per ChildId.
+    Child ids must lie in [0, nc) and gift ids in [0, ng) (where given); every
+    child needs a gift."""
     import pandas as pd
     sub = pd.read_csv(path)
     child = sub["ChildId"].to_numpy()
     gift = sub["GiftId"].to_numpy()
     n = int(nc if nc is not None else child.max() + 1)
+    if child.size and (child.min() < 0 or child.max() >= n):
+        raise ValueError(f"{path}: ChildId outside [0, {n})")
+    hi = ng if ng is not None else np.iinfo(np.int16).max + 1
+    if gift.size and (gift.min() < 0 or gift.max() >= hi):
+        raise ValueError(f"{path}: GiftId outside [0, {hi})")
     types = np.full(n, -1, dtype=np.int16)
     types[child] = gift
     if (types < 0).any():

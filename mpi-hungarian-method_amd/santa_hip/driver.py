@@ -115,10 +115,19 @@ def exchange(engine, world: World, mode: int, rows: torch.Tensor, n: int, B: int
 def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, n: int = 256,
                blocks_per_round: int | None = None, seed: int = 2017, max_rounds: int = 100,
                accept: str | None = None, patience: int = 3, world: World | None = None,
-               on_round=None, score0: float | None = None) -> LoopResult:
-    """The reference's while-loop; `types` (device int16 [nc]) is updated in place."""
+               on_round=None, score0: float | None = None,
+               check_disjoint: bool = False) -> LoopResult:
+    """The reference's while-loop; `types` (device int16 [nc]) is updated in place.
+
+    accept: "always" (mpi_single.py: the new state is always kept) or
+    "improve" (mpi_twins.py: kept only if the score improves); default by mode.
+    check_disjoint: debug mode, assert that each round's blocks are a
+    partition (no child in two blocks; twins: no pair overlap), which the
+    in-place apply relies on."""
     world = world or World()
     accept = accept or ("always" if mode == _lib.SH_MODE_SINGLE else "improve")
+    if accept not in ("always", "improve"):
+        raise ValueError(f"accept must be 'always' or 'improve', not {accept!r}")
     _, _, _, nb = engine.geometry(mode, n)
     B = nb if blocks_per_round is None else int(blocks_per_round)
     if B < 1 or B > nb:
@@ -140,6 +149,8 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
     for rnd in range(max_rounds):
         t0 = time.perf_counter()
         rows = engine.sample_blocks(mode, n, B, seed, rnd)
+        if check_disjoint:
+            assert_disjoint(rows, mode)
         if backup is not None:
             backup.copy_(types)
         if b1 > b0:
@@ -170,6 +181,15 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
             break
     res.best_score = best
     return res
+
+
+def assert_disjoint(rows: torch.Tensor, mode: int) -> None:
+    """Debug check: the round's blocks share no child.  Twins
+    rows are first twins c, whose pair is (c, c+1)."""
+    r = rows.reshape(-1).long()
+    kids = torch.cat([r, r + 1]) if mode == _lib.SH_MODE_TWINS else r
+    if torch.unique(kids).numel() != kids.numel() or bool((r < 0).any()):
+        raise AssertionError("blocks of a round are not disjoint (the in-place apply needs a partition)")
 
 
 class GPUEngine:
@@ -214,7 +234,9 @@ def my_optimizer(subm, score_org, comm=None, rank: int = 0, size: int = 1, gift_
     for singles, twin pairs for twins.  Returns the improved DataFrame."""
     from .context import SantaGPU
     ctx = SantaGPU(child_data, gift_data, child_data.shape[0] // gift_data.shape[0], device)
-    types_np = np.full(ctx.nc, -1, dtype=np.int16)
+    # int64 first: a GiftId outside [0, ng) (or a child left at -1) must raise,
+    # as the reference's indexing does, not wrap into int16
+    types_np = np.full(ctx.nc, -1, dtype=np.int64)
     types_np[subm["ChildId"].to_numpy()] = subm["GiftId"].to_numpy()
     types = ctx.upload_types(types_np)
     m = _lib.SH_MODE_SINGLE if mode == "single" else _lib.SH_MODE_TWINS
@@ -241,6 +263,14 @@ def main(argv=None) -> int:
                     help="'full' (all disjoint blocks), 'ranks' (reference: one per rank) or an int")
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--patience", type=int, default=3)
+    ap.add_argument("--accept", choices=["always", "improve"], default=None,
+                    help="keep every round (mpi_single.py) or only improving ones (mpi_twins.py); "
+                         "default by mode")
+    ap.add_argument("--checkpoint-every", type=int, default=0, metavar="K",
+                    help="rank 0 rewrites --out every K rounds (the reference: every round, "
+                         "mpi_single.py:177)")
+    ap.add_argument("--check-disjoint", action="store_true",
+                    help="debug: assert every round's blocks are a partition")
     ap.add_argument("--seed", type=int, default=2017)
     ap.add_argument("--wishlist", help="child_wishlist_v2.csv (default: synthetic data)")
     ap.add_argument("--goodkids", help="gift_goodkids_v2.csv")
@@ -262,26 +292,34 @@ def main(argv=None) -> int:
     dev = torch.cuda.current_device()
     if args.wishlist:
         wish, good = D.read_wishlist(args.wishlist), D.read_goodkids(args.goodkids)
-        types0 = D.read_submission(args.init, wish.shape[0])
+        types0 = D.read_submission(args.init, wish.shape[0], good.shape[0])
         nq = wish.shape[0] // good.shape[0]
     else:
         sd = D.synthetic(args.synthetic_seed)
         wish, good, types0, nq = sd.wish, sd.goodkids, sd.types, sd.nq
         if args.init:
-            types0 = D.read_submission(args.init, wish.shape[0])
+            types0 = D.read_submission(args.init, wish.shape[0], good.shape[0])
     ctx = SantaGPU(wish, good, nq, dev)
     types = ctx.upload_types(types0)
     mode = _lib.SH_MODE_SINGLE if args.mode == "single" else _lib.SH_MODE_TWINS
     bpr = None if args.blocks_per_round == "full" else (
         world.size if args.blocks_per_round == "ranks" else int(args.blocks_per_round))
 
+    if args.checkpoint_every and not args.out:
+        ap.error("--checkpoint-every needs --out")
+
     def log(st: RoundStats):
         if world.rank == 0:
             print(json.dumps(st.__dict__), flush=True)
+            # the reference's per-round checkpoint (mpi_single.py:176-177), taken
+            # after the round's timing: the accepted state is the current one
+            if args.checkpoint_every and (st.round + 1) % args.checkpoint_every == 0:
+                D.write_submission(args.out, types.cpu().numpy())
 
     res = run_rounds(GPUEngine(ctx), types, mode=mode, n=args.block_size, blocks_per_round=bpr,
-                     seed=args.seed, max_rounds=args.rounds, patience=args.patience, world=world,
-                     on_round=log)
+                     seed=args.seed, max_rounds=args.rounds, accept=args.accept,
+                     patience=args.patience, world=world, on_round=log,
+                     check_disjoint=args.check_disjoint)
     if world.rank == 0:
         print(json.dumps({"rounds": res.rounds, "blocks": res.blocks_solved,
                           "best_score": res.best_score}), flush=True)

@@ -24,6 +24,7 @@ def _p(t):
 
 
 INT64_COST_LIMIT = 1 << 50  # |C| bound that keeps every SAP value < 2^62 (n <= 1024)
+EXACT_INT_LIMIT = 1 << 53   # float64 holds every integer below this exactly
 
 
 def solve_batched(C: torch.Tensor, with_cost: bool = True, flags: int = 0):
@@ -75,8 +76,9 @@ def linear_sum_assignment(cost_matrix, maximize: bool = False, device: int | str
     """scipy.optimize.linear_sum_assignment for one matrix, solved on the GPU.
 
     Square matrices only (the reference's blocks are square).  Integer
-    matrices are solved in exact int64; anything else in float64 with
-    scipy's operation order."""
+    matrices whose sums stay below 2^53 are solved in exact int64 (where
+    scipy's float64 arithmetic is exact too); anything else in float64 with
+    scipy's operation order, so the permutation is scipy's either way."""
     C = np.asarray(cost_matrix)
     if C.ndim != 2:
         raise ValueError("expected a matrix (2-D array), got a %r array" % (C.shape,))
@@ -87,11 +89,22 @@ def linear_sum_assignment(cost_matrix, maximize: bool = False, device: int | str
         return np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.int64)
     if n > _lib.SH_MAX_N:
         raise ValueError(f"n = {n} > {_lib.SH_MAX_N}")
+    dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+    if C.dtype == np.bool_:
+        C = C.astype(np.int64)
+    if np.issubdtype(C.dtype, np.unsignedinteger):
+        # negating an unsigned array wraps: widen first (uint64 beyond int64 -> float64)
+        C = C.astype(np.int64) if (C.size == 0 or int(C.max()) <= np.iinfo(np.int64).max) \
+            else C.astype(np.float64)
     if maximize:
         C = -C
-    dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
-    if (np.issubdtype(C.dtype, np.integer) or C.dtype == np.bool_) and \
-            (C.size == 0 or int(np.abs(C.astype(np.int64)).max()) < INT64_COST_LIMIT):
+    # scipy solves in float64.  Integer input is solved in exact int64, which
+    # makes scipy's decisions only while every value it forms is an integer
+    # below 2^53 (no float64 rounding); duals and path lengths stay within a few
+    # n * max|C|, so 4 (n + 1) max|C| < 2^53 is a safe bound.
+    # Wider ranges take the float64 replay of scipy's own arithmetic.
+    if np.issubdtype(C.dtype, np.integer) and \
+            (C.size == 0 or 4 * (n + 1) * int(np.abs(C.astype(np.int64)).max()) < EXACT_INT_LIMIT):
         Ct = torch.from_numpy(np.ascontiguousarray(C, dtype=np.int64)).to(dev)
     else:
         Cf = np.ascontiguousarray(C, dtype=np.float64)

@@ -300,8 +300,21 @@ def make_trajectory(sd: D.SantaData, mode: str, P: int, n: int, rounds: int, see
     gift_ids = np.array([[g] * nq for g in range(ng)]).flatten()
     records = []
     orig_score = ns["avg_normalized_happiness"]
+    csv_name = "improved_sub.csv" if mode == "single" else "improved_twins.csv"
+
+    def csv_digest():
+        """The reference's own checkpoint of the last round (rank 0's
+        subm_best[['ChildId','GiftId']].to_csv(..., index=False),
+        mpi_single.py:177 / mpi_twins.py:183), as sha256 + size."""
+        if not os.path.exists(csv_name):
+            return None
+        data = open(csv_name, "rb").read()
+        return {"sha256": hashlib.sha256(data).hexdigest(), "bytes": len(data)}
 
     def scored(pred, child_pref, gift_pref):
+        # the CSV on disk now is the previous round's checkpoint
+        if len(records) > 1 and "csv" not in records[-1]:
+            records[-1]["csv"] = csv_digest()
         s = orig_score(pred, child_pref, gift_pref)
         records.append({"score": float(s), "types_sha": sha(pred[:, 1].astype(np.int16))})
         return s
@@ -375,6 +388,8 @@ def make_trajectory(sd: D.SantaData, mode: str, P: int, n: int, rounds: int, see
         except _Stop:
             finished = False
         finally:
+            if len(records) > 1 and "csv" not in records[-1]:
+                records[-1]["csv"] = csv_digest()
             os.chdir(cwd)
     out_obj = {"mode": mode, "P": P, "n": n, "seed": seed, "rounds": rounds,
                "data": {"seed": 2017, "wish_sha": sha(sd.wish), "good_sha": sha(sd.goodkids),

@@ -167,3 +167,45 @@ def test_hash_cost_host_mirror_shape():
     assert C.shape == (16, 16) and C.min() >= 0 and C.max() < 100
     assert np.array_equal(C, S.hash_matrix(7, 0, 16, 100))
     assert not np.array_equal(C, S.hash_matrix(7, 1, 16, 100))
+
+
+def test_gift_types_outside_range_are_rejected_on_the_host(tmp_path):
+    """Gift types index on-chip tables in the kernels: the host refuses a
+    type outside [0, ng) (the reference's numpy indexing raises IndexError)
+    before anything reaches the device."""
+    from santa_hip.context import check_types
+    check_types(np.array([0, 5, 9], dtype=np.int64), 10)
+    for bad in ([0, 10, 3], [-1, 2, 3], [0, 1, 40000]):
+        with pytest.raises(ValueError):
+            check_types(np.array(bad, dtype=np.int64), 10)
+    p = tmp_path / "sub.csv"
+    open(p, "w").write("ChildId,GiftId\n0,1\n1,20\n2,3\n")
+    assert np.array_equal(D.read_submission(str(p), 3), [1, 20, 3])
+    with pytest.raises(ValueError):
+        D.read_submission(str(p), 3, ng=20)
+    open(p, "w").write("ChildId,GiftId\n0,1\n5,2\n")
+    with pytest.raises(ValueError):
+        D.read_submission(str(p), 3)
+
+
+def test_lsap_front_end_routes_wide_integers_to_float64(monkeypatch):
+    """linear_sum_assignment solves integers in int64 only while scipy's
+    float64 arithmetic on them is exact; wider ranges and unsigned input
+    with maximize=True take the float64 replay (no GPU call: the solver is
+    stubbed and the dtype it receives is recorded)."""
+    import torch
+    from santa_hip import lsap
+    seen = []
+
+    def fake(C, with_cost=True, flags=0):
+        seen.append(C.dtype)
+        B, n, _ = C.shape
+        return torch.arange(n, dtype=torch.int32).repeat(B, 1), None
+
+    monkeypatch.setattr(lsap, "solve_batched", fake)
+    monkeypatch.setattr(torch.Tensor, "to", lambda self, *a, **k: self)
+    lsap.linear_sum_assignment(np.array([[1, 2], [3, 4]]), device="cpu")
+    lsap.linear_sum_assignment(np.array([[1 << 50, 2], [3, 4]]), device="cpu")
+    lsap.linear_sum_assignment(np.array([[1, 2], [3, 4]], dtype=np.uint8), maximize=True, device="cpu")
+    lsap.linear_sum_assignment(np.array([[0.5, 2], [3, 4]]), device="cpu")
+    assert seen == [torch.int64, torch.float64, torch.int64, torch.float64]

@@ -109,3 +109,27 @@ def test_all_gather_sends_rccl_dtypes(monkeypatch):
     all_gather_flat(out, inp)
     assert seen == [(torch.uint8, torch.uint8)]
     assert torch.equal(out, torch.cat([inp, inp]))
+
+
+def test_accept_modes_and_disjoint_check():
+    """--accept overrides the mode's rule (always-keep vs keep-if-improved),
+    an unknown rule is refused, and the debug partition check passes on the
+    sampler's blocks but catches an overlap."""
+    from cpu_engine import CPUOracleEngine
+    from santa_hip.driver import assert_disjoint
+    sd = D.synthetic(**SMALL)
+    eng = CPUOracleEngine(sd.wish, sd.goodkids, sd.nq)
+    for accept in ("always", "improve"):
+        t = torch.from_numpy(sd.types.copy())
+        res = run_rounds(eng, t, mode=_lib.SH_MODE_SINGLE, n=64, seed=3, max_rounds=2,
+                         accept=accept, world=World(), check_disjoint=True)
+        assert res.rounds == 2
+        assert all(st.accepted for st in res.history) or accept == "improve"
+    with pytest.raises(ValueError):
+        run_rounds(eng, torch.from_numpy(sd.types.copy()), mode=0, n=64, max_rounds=1, accept="maybe")
+    rows = eng.sample_blocks(_lib.SH_MODE_TWINS, 16, 4, 1, 0)
+    assert_disjoint(rows, _lib.SH_MODE_TWINS)
+    with pytest.raises(AssertionError):
+        assert_disjoint(torch.cat([rows, rows[:1]]), _lib.SH_MODE_TWINS)
+    with pytest.raises(AssertionError):  # pairs (c, c+1) and (c+1, c+2) overlap
+        assert_disjoint(torch.tensor([11, 12], dtype=torch.int32), _lib.SH_MODE_TWINS)

@@ -257,22 +257,36 @@ def test_avg_normalized_happiness_api(sh, full_data):
 
 # --------------------------------------------------------------------------- driver
 @pytest.mark.parametrize("mode", ["single", "twins"])
-def test_trajectory_gpu_matches_reference(sh, ctx, full_data, mode):
+def test_trajectory_gpu_matches_reference(sh, ctx, full_data, mode, tmp_path):
+    """The reference's my_optimizer (3 rounds, P blocks per round) replayed
+    on the GPU: scores, states and the per-round checkpoint CSV (byte-
+    identical to the reference's to_csv, mpi_single.py:177) all equal."""
+    import hashlib
+
+    from santa_hip import data as D
     from santa_hip.driver import GPUEngine, World, run_rounds
     g = golden_json(f"trajectory_{mode}.json")
     types = ctx.upload_types(full_data.types)
     shas = []
+    csvs = []
 
     class Rec(GPUEngine):
         def score_sums(self, t):
             shas.append(sha(t.cpu().numpy()))
             return super().score_sums(t)
 
+    def checkpoint(st):
+        p = tmp_path / f"r{st.round}.csv"
+        D.write_submission(str(p), types.cpu().numpy())
+        data = open(p, "rb").read()
+        csvs.append({"sha256": hashlib.sha256(data).hexdigest(), "bytes": len(data)})
+
     m = 0 if mode == "single" else 1
     res = run_rounds(Rec(ctx), types, mode=m, n=g["n"], blocks_per_round=g["P"], seed=g["seed"],
-                     max_rounds=g["rounds"], world=World(), score0=g["score0"])
+                     max_rounds=g["rounds"], world=World(), score0=g["score0"], on_round=checkpoint)
     assert [st.score for st in res.history] == [r["score"] for r in g["per_round"]]
     assert shas == [r["types_sha"] for r in g["per_round"]]
+    assert csvs == [r["csv"] for r in g["per_round"]]
 
 
 def test_optimize_block_api(sh, full_data, santa_blocks):
@@ -516,3 +530,107 @@ def test_santa_edge_block_sizes_vs_oracle(sh, ctx, full_data, mode, n, B):
         assert np.array_equal(types.cpu().numpy(), t_host), fl
         assert delta.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]], fl
         assert ctx.error_flags() == 0
+
+
+# --------------------------------------------------------------------------- config 4 on the HIP path
+@pytest.mark.parametrize("mode,rounds", [(0, 3), (1, 3)])
+def test_two_ranks_on_the_hip_path_equal_one_rank(sh, ctx, full_data, mode, rounds):
+    """Config 4's sharding + exchange through GPUEngine: two ranks (one
+    process each, both on cuda:0, gloo all-gather) run full rounds (3730
+    singles / 78 twin blocks) and end with the single-rank run's type vector
+    and every per-round (S_child, S_gift), bit for bit."""
+    import socket
+
+    import torch.multiprocessing as mp
+    from multirank_gpu import rank_main
+    from santa_hip.driver import GPUEngine, World, run_rounds
+    types = ctx.upload_types(full_data.types)
+    sums = []
+
+    class Rec(GPUEngine):
+        def score_sums(self, t):
+            s = super().score_sums(t)
+            sums.append(s[:2])
+            return s
+
+    res = run_rounds(Rec(ctx), types, mode=mode, n=256, seed=41, max_rounds=rounds, patience=100,
+                     world=World())
+    want = types.cpu().numpy()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(rank_main, args=(2, port, mode, 256, rounds, 41, out), nprocs=2, join=True)
+    for r in range(2):
+        t, sm, scores, flags = out[r]
+        assert flags == 0
+        assert np.array_equal(t, want), f"rank {r} state differs"
+        assert sm == sums, f"rank {r} per-round sums differ"
+        assert scores == [st.score for st in res.history]
+
+
+def test_bench_launches_n_ranks(sh):
+    """`bench.py --gpus 2` started by hand launches its two ranks itself and
+    reports n_gpus = 2 (here both on the one GPU of the box, over gloo)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1", "--one-device", "--dist-backend", "gloo", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["config"]["blocks_per_round"] == 3730
+
+
+# --------------------------------------------------------------------------- input validation
+@pytest.mark.parametrize("mode,n,fl", [(0, 256, 128), (0, 256, 8), (0, 256, 32), (0, 256, 16),
+                                       (1, 256, 0), (0, 300, 0), (1, 300, 0)])
+def test_gift_type_out_of_range_is_flagged_not_used(sh, ctx, full_data, mode, n, fl):
+    """A current gift type outside [0, ng) in a block (it would index the
+    kernels' on-chip tables) makes every kernel design skip that block and
+    raise SH_ERRF_TYPE; the other blocks of the launch are solved."""
+    from santa_hip import _lib
+    B = 3
+    rows = ctx.sample_blocks(mode, n, B, 5, 1)
+    t = full_data.types.copy()
+    bad_child = int(rows[n + 7])        # a child of block 1
+    t[bad_child] = full_data.ng         # one past the last gift type
+    if mode == 1:
+        t[bad_child + 1] = full_data.ng
+    types = torch.from_numpy(t).cuda()  # (bypasses upload_types' host check on purpose)
+    ctx.error_flags()
+    ctx.solve_blocks(mode, rows, n, types, flags=fl)
+    flags = ctx.error_flags()
+    assert flags & _lib.SH_ERRF_TYPE, flags
+    got = types.cpu().numpy()
+    r = rows.cpu().numpy().reshape(B, n)
+    assert np.array_equal(got[r[1]], t[r[1]])                       # skipped whole
+    t_host = full_data.types.copy()
+    ocol, _ = oracle.round_blocks(mode, full_data.wish, t_host, r[[0, 2]], ng=full_data.ng)
+    assert np.array_equal(got[r[[0, 2]].reshape(-1)], t_host[r[[0, 2]].reshape(-1)])
+    with pytest.raises(ValueError):
+        ctx.upload_types(t)
+
+
+def test_context_on_a_second_device(sh, full_data):
+    """A context bound to device 1 works while device 0 is current (the C-ABI
+    switches to the context's device and back)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one visible GPU")
+    c1 = sh.SantaGPU.from_data(full_data, 1)
+    torch.cuda.set_device(0)
+    types = c1.upload_types(full_data.types)
+    rows = c1.sample_blocks(0, 256, 8, 3, 0)
+    c1.solve_blocks(0, rows, 256, types)
+    assert torch.cuda.current_device() == 0
+    t_host = full_data.types.copy()
+    oracle.round_blocks(0, full_data.wish, t_host, rows.cpu().numpy().reshape(8, 256), ng=full_data.ng)
+    assert np.array_equal(types.cpu().numpy(), t_host)
+    assert c1.error_flags() == 0

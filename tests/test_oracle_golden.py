@@ -9,6 +9,8 @@ Pins the oracle before it is trusted as the GPU path's checker:
                          (mpi_single.py:13-83) on the full synthetic instance;
   * trajectory_*.json  — the reference's my_optimizer run for 3 rounds.
 """
+import hashlib
+
 import numpy as np
 import pytest
 
@@ -129,18 +131,36 @@ def test_score_matches_reference(full_data):
     assert s == base["score"]
 
 
+def csv_digest(path) -> dict:
+    data = open(path, "rb").read()
+    return {"sha256": hashlib.sha256(data).hexdigest(), "bytes": len(data)}
+
+
 @pytest.mark.parametrize("mode", ["single", "twins"])
-def test_trajectory_matches_reference(full_data, mode):
+def test_trajectory_matches_reference(full_data, mode, tmp_path):
     """run_rounds (the product driver) on the CPU oracle engine replays the
-    reference's my_optimizer: same scores, bit for bit, same states."""
+    reference's my_optimizer: same scores, bit for bit, same states, and the
+    checkpoint CSV santa_hip.data.write_submission writes after each round is
+    byte-identical to the reference's own subm_best[['ChildId','GiftId']]
+    .to_csv(..., index=False) of that round (mpi_single.py:177,
+    mpi_twins.py:183; sha256 recorded by make_golden.py)."""
+    from santa_hip import data as D
     g = golden_json(f"trajectory_{mode}.json")
     eng = CPUOracleEngine(full_data.wish, full_data.goodkids, full_data.nq)
     import torch
     types = torch.from_numpy(full_data.types.copy())
     m = _lib.SH_MODE_SINGLE if mode == "single" else _lib.SH_MODE_TWINS
+    csvs = []
+
+    def checkpoint(st):
+        p = tmp_path / f"r{st.round}.csv"
+        D.write_submission(str(p), types.numpy())
+        csvs.append(csv_digest(p))
+
     res = run_rounds(eng, types, mode=m, n=g["n"], blocks_per_round=g["P"], seed=g["seed"],
-                     max_rounds=g["rounds"], world=World(), score0=g["score0"])
+                     max_rounds=g["rounds"], world=World(), score0=g["score0"], on_round=checkpoint)
     assert res.rounds == len(g["per_round"])
-    for st, want, log in zip(res.history, g["per_round"], eng.score_log):
+    for st, want, log, c in zip(res.history, g["per_round"], eng.score_log, csvs):
         assert st.score == want["score"]
         assert log[2] == want["types_sha"]
+        assert c == want["csv"], st.round

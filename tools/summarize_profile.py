@@ -6,6 +6,7 @@ HBM bytes per launch from FETCH_SIZE / WRITE_SIZE (KB, x1024), and the SQ
 counters per wave and per Dijkstra step of the block kernel."""
 import csv
 import glob
+import hashlib
 import json
 import os
 import shutil
@@ -46,7 +47,9 @@ def main(src, tag, root):
         for r in rows:
             trace[short(r["Kernel_Name"])].append(
                 (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-    out = {"tag": tag, "trace_ms": {k: {"calls": len(v), "avg_ms": sum(v) / len(v),
+    src = os.path.join(root, "mpi-hungarian-method_amd", "csrc", "santa_hip.hip")
+    out = {"tag": tag, "source_sha16": hashlib.sha256(open(src, "rb").read()).hexdigest()[:16],
+           "trace_ms": {k: {"calls": len(v), "avg_ms": sum(v) / len(v),
                                          "min_ms": min(v), "max_ms": max(v)}
                                      for k, v in trace.items()}}
     # the bench's timed rounds: launches [warmup, warmup + steps) of the block
