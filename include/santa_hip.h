@@ -57,6 +57,9 @@ extern "C" {
                                    bits: built, solved, done) into d_steps */
 #define SH_FLAG_SP_TILE 128u    /* force the one-wave sparse kernel (the
                                    throughput design) even for few blocks  */
+#define SH_FLAG_SP1 256u        /* force the sparse kernel with LDS hit lists
+                                   (santa_sp_kernel) instead of the register
+                                   hit tile (A/B; identical results)       */
 
 /* Kernel designs sh_solve_blocks can dispatch to (sh_solve_design).        */
 #define SH_DESIGN_SPARSE 0   /* one wave per block, hit lists in LDS        */
@@ -65,6 +68,7 @@ extern "C" {
 #define SH_DESIGN_VT_TILE 3  /* 4 waves, register tile (A/B; nc > 2^20)     */
 #define SH_DESIGN_TWINS 4    /* twins n <= 256: 4 waves, code-pair tile     */
 #define SH_DESIGN_LARGE 5    /* n > 256: row rebuilt from the wishlist      */
+#define SH_DESIGN_SPARSE2 6  /* one wave per block, hit tile in VGPRs       */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024

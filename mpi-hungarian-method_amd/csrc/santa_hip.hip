@@ -2274,6 +2274,639 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Sparse register-tile design (singles, n <= 256): the throughput path.
+//
+// santa_sp_kernel's algorithm, decisions and Dijkstra step, with the per-row
+// hit lists held in VGPRs instead of LDS.  The solve kernel then needs ~8 KB
+// of LDS per block instead of ~20 KB, so LDS no longer caps a CU at 8 blocks.
+// Two launches per round:
+//   santa_tile_kernel  builds every block's hit tile (the column sort and the
+//                      hit-list build of santa_sp_kernel, 8 rows at a time
+//                      through a small LDS list) and stores it to a per-block
+//                      record in HBM (~18 KB per block, ~70 MB per 3730-block
+//                      round: ~25 us of HBM time against ~2 ms of solving);
+//   santa_sp2_kernel   loads the tile into VGPRs (coalesced 16-byte loads)
+//                      and runs the solve with the build's registers free.
+// Tile layout: two u32x32 vectors T0, T1 (64 VGPRs); row i lives in VGPR
+// q = i >> 2 (T0 for q < 32, else T1), lanes 32L..32L+31 with
+// L = (i >> 1) & 1, 16-bit half H = i & 1; the row's entry x is in lane
+// 32L + x.  Entry = slot (9 bits: the column's rowc slot, or 256 + x = the
+// lane's dump slot) | a << 9 with a = n_wish + 1 - code (cost -a * 2^32;
+// 0 = unused entry, SP2_MARK = overflow marker).  A row with more than 32 hits
+// keeps 31 in the tile, the marker in entry 31 and the rest in an overflow
+// list (ovf, ranges ovfr[i] = start | count << 16): ~13 % of rows on
+// Kaggle-shaped data, one extra LDS round trip on their steps.  A block whose
+// overflow does not fit is left to the fallback launch (santa_vt_kernel).
+// A Dijkstra step reads its row with one indexed VGPR move (s_set_gpr_idx)
+// instead of a range lookup and an LDS read.
+// ---------------------------------------------------------------------------
+constexpr int SP2_SUB_CAP = 512;   // hit entries of one 8-row build sub-round
+constexpr uint32_t SP2_MARK = 127; // overflow marker in the `a` field (n_wish <= 126)
+constexpr int SP2_OVF_CAP = 512;   // overflow entries per block
+// per-block record in HBM (bytes): tile | ovf | ovfr | own | status
+constexpr size_t SP2_REC_TILE = 0;
+constexpr size_t SP2_REC_OVF = 64 * 64 * 4;
+constexpr size_t SP2_REC_OVFR = SP2_REC_OVF + SP2_OVF_CAP * 2;
+constexpr size_t SP2_REC_OWN = SP2_REC_OVFR + 256 * 4;
+constexpr size_t SP2_REC_STATUS = SP2_REC_OWN + 256;
+constexpr size_t SP2_REC = SP2_REC_STATUS + 128;  // 18816 bytes
+
+struct TileLds {
+  size_t own, csort, thead, off, hits, total;
+};
+
+__host__ __device__ __forceinline__ TileLds tile_lds_layout(int ng) {
+  TileLds L;
+  size_t o = 0;
+  L.own = o;    o += 256;                      // code(i, i): row i's own (old) gift
+  L.csort = o;  o += 272;                      // columns sorted by gift type (+ pad)
+  L.thead = o;  o += r16((size_t)ng * 4);      // counting-sort counters, then the type table
+  L.off = o;    o += 32;                       // hit-list offsets of the sub-round's 8 rows
+  L.hits = o;   o += (SP2_SUB_CAP + 2 * 64) * 2;  // the sub-round's hit list + a dump per lane
+  L.total = o;
+  return L;
+}
+
+// dword index of (VGPR q, lane) in a tile record: 4 consecutive VGPRs of a
+// lane are one 16-byte word, lanes contiguous (coalesced 16-byte loads)
+__device__ __forceinline__ int tile_word(int q, int lane) { return ((q >> 2) * 64 + lane) * 4 + (q & 3); }
+
+// hit-list entry of the build (slot | (code - nw1) << 8) -> tile entry (slot | a << 9)
+__device__ __forceinline__ uint32_t tile_entry(uint32_t h) {
+  return (h & 0xFFu) | ((uint32_t)(-(int)(int8_t)(h >> 8)) << 9);
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(WAVE) void santa_tile_kernel(SantaArgs a, unsigned char *rec_all) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int n = a.n;
+  const TileLds L = tile_lds_layout(a.ng);
+  uint8_t *own = smem + L.own;
+  uint8_t *csort = smem + L.csort;
+  uint32_t *thead = (uint32_t *)(smem + L.thead);
+  uint32_t *tcnt = thead;  // counting-sort counters, turned into the type table in place
+  uint16_t *off_l = (uint16_t *)(smem + L.off);
+  uint16_t *hits = (uint16_t *)(smem + L.hits);
+  unsigned char *rec = rec_all + (size_t)b * SP2_REC;
+  uint32_t *rtile = (uint32_t *)(rec + SP2_REC_TILE);
+  uint16_t *rovf = (uint16_t *)(rec + SP2_REC_OVF);
+  uint32_t *rovfr = (uint32_t *)(rec + SP2_REC_OVFR);
+  int32_t *status = (int32_t *)(rec + SP2_REC_STATUS);
+
+  // -- rows (lane l owns rows 4l..4l+3), range check --------------------------------
+  int child[4];
+  int bad = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = 4 * lane + k;
+    child[k] = (r < n) ? a.rows[(size_t)b * n + r] : 0;
+    bad |= (r < n) && ((child[k] < 0) || (child[k] >= a.nc));
+  }
+  if (__any(bad)) {
+    if (lane == 0) {
+      atomicOr(a.err, SH_ERRF_ROWS);
+      *status = 1;  // skip
+    }
+    return;
+  }
+  // -- columns sorted by gift type (counting sort, as santa_sp_kernel) ---------------
+  for (int t = lane; t < a.ng; t += WAVE) tcnt[t] = 0u;
+  ((uint32_t *)own)[lane] = 0;
+  int myt[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) myt[k] = (4 * lane + k < n) ? a.types[child[k]] : -1;
+  {  // the types index LDS tables: reject the block if one is out of range
+    int badt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) badt |= (4 * lane + k < n) && (myt[k] < 0 || myt[k] >= a.ng);
+    if (__any(badt)) {
+      if (lane == 0) {
+        atomicOr(a.err, SH_ERRF_TYPE);
+        *status = 1;
+      }
+      return;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (myt[k] >= 0) atomicAdd(&tcnt[myt[k]], 1u << 16);
+  __syncthreads();
+  int big = 0;
+  {  // exclusive scan of the counts over types -> start of each type in csort
+    const int per = (a.ng + WAVE - 1) / WAVE;
+    const int t0s = lane * per, t1s = min(a.ng, t0s + per);
+    uint32_t sum = 0;
+    for (int t = t0s; t < t1s; ++t) sum += tcnt[t] >> 16;
+    uint32_t run = wave_incl_scan_u32(sum) - sum;
+    for (int t = t0s; t < t1s; ++t) {
+      const uint32_t h = tcnt[t];
+      tcnt[t] = h | run;  // low half: fill cursor
+      big |= (h >> 16) >= 255u;
+      run += h >> 16;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (myt[k] >= 0) csort[atomicAdd(&tcnt[myt[k]], 1u) & 0xFFFFu] = (uint8_t)rowc_slot(4 * lane + k);
+  __syncthreads();
+  {  // per type, in place: c0 | c1 << 8 | (count <= 3 ? c2 : start in csort) << 16 | count << 24
+    const int per = (a.ng + WAVE - 1) / WAVE;
+    const int t0s = lane * per, t1s = min(a.ng, t0s + per);
+    for (int t = t0s; t < t1s; ++t) {
+      const uint32_t h = tcnt[t];
+      const uint32_t c = h >> 16, e = (h & 0xFFFFu) - c;  // start in csort
+      const uint32_t x2 = c <= 3u ? (uint32_t)csort[e + 2] : e;
+      thead[t] = c ? ((uint32_t)csort[e] | ((uint32_t)csort[e + 1] << 8) | (x2 << 16) |
+                      (min(c, 255u) << 24))
+                   : 0u;
+    }
+  }
+  __syncthreads();
+
+  // -- the tile, 8 rows per sub-round, 8 lanes per row -------------------------------
+  // As santa_sp_kernel: lane 8q+j takes wishlist chunks [j*ncq, (j+1)*ncq) of row
+  // s0+q, looks them up in the type table, and one wave scan places the hits in
+  // the sub-round's LDS list (rows in order).  The list then goes to the tile:
+  // lane 32L+x takes entry x of the two rows of each VGPR it holds.
+  const int nw = a.n_wish;
+  constexpr int LPR = 8;                         // lanes per row
+  constexpr int RPS = WAVE / LPR;                // rows per sub-round
+  constexpr int MAXQ = 4;                        // chunks per lane (n_wish <= 127)
+  const int nch = (nw + 3) >> 2;
+  const int ncq = (nch + LPR - 1) / LPR;
+  const int qr = lane / LPR, qj = lane % LPR;
+  bool fits = !__any(big);
+  auto load_chunk = [&](const int16_t *src, int c) -> uint2 {
+    uint2 q;
+    if constexpr (VEC) {
+      q = *(const uint2 *)(src + 4 * min(c, nch - 1));
+    } else {
+      uint32_t g4[4];
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int r = 4 * c + z;
+        g4[z] = (r < nw) ? (uint16_t)src[min(r, nw - 1)] : 0xFFFFu;
+      }
+      q.x = g4[0] | (g4[1] << 16);
+      q.y = g4[2] | (g4[3] << 16);
+    }
+    return q;
+  };
+  auto gift_of = [](const uint2 &q, int z) -> int {
+    return (int)(int16_t)(((z < 2 ? q.x : q.y) >> (16 * (z & 1))) & 0xFFFFu);
+  };
+  const int dump = SP2_SUB_CAP + 2 * lane;
+  const int cb = qj * ncq;
+  int ct[4];  // child id | (own type + 1) << 20 (children < 2^20, types < 1023)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ct[k] = child[k] | ((myt[k] + 1) << 20);
+  auto row_child = [&](int row, int &chd, int &mt) {
+    int x = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c2 = __shfl(ct[k], (row >> 2) & 63, WAVE);
+      x = ((row & 3) == k) ? c2 : x;
+    }
+    chd = x & 0xFFFFF;
+    mt = (x >> 20) - 1;
+  };
+  int obase = 0;  // overflow entries used so far
+  const int Lh = lane >> 5, x31 = lane & 31;
+  uint2 qn[MAXQ];
+  int chdn, mtn;
+  row_child(qr, chdn, mtn);
+#pragma unroll
+  for (int t = 0; t < MAXQ; ++t) qn[t] = load_chunk(a.wish + (size_t)chdn * nw, cb + t);
+#pragma unroll 1
+  for (int s0 = 0; s0 < n && fits; s0 += RPS) {
+    const int row = s0 + qr;
+    const bool lr = row < n;
+    const int mt = mtn;
+    uint2 q[MAXQ];
+#pragma unroll
+    for (int t = 0; t < MAXQ; ++t) q[t] = qn[t];
+    if (s0 + RPS < n) {
+      row_child(s0 + RPS + qr, chdn, mtn);
+#pragma unroll
+      for (int t = 0; t < MAXQ; ++t) qn[t] = load_chunk(a.wish + (size_t)chdn * nw, cb + t);
+    }
+    uint32_t hv[MAXQ][4];
+    int cnt = 0;
+    uint32_t ownc = 0;
+#pragma unroll
+    for (int t = 0; t < MAXQ; ++t) {
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int g = gift_of(q[t], z);
+        const bool ok = lr && (t < ncq) && (cb + t < nch) && (g >= 0);
+        const uint32_t h = thead[ok ? g : 0];
+        hv[t][z] = ok ? h : 0u;
+        cnt += (int)(hv[t][z] >> 24);
+        ownc = (ok && g == mt) ? (uint32_t)(4 * (cb + t) + z + 1) : ownc;
+      }
+    }
+    const uint32_t incl = wave_incl_scan_u32((uint32_t)cnt);
+    const int total = __builtin_amdgcn_readlane((int)incl, 63);
+    if (total > SP2_SUB_CAP) {
+      fits = false;
+      break;
+    }
+    const int start = (int)incl - cnt;
+    if (qj == 0) off_l[qr] = (uint16_t)start;
+    if (lane == 0) off_l[RPS] = (uint16_t)total;
+    if (ownc) own[row] = (uint8_t)ownc;
+    int p = start;
+    bool many = false;
+#pragma unroll
+    for (int t = 0; t < MAXQ; ++t)
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const uint32_t h = hv[t][z];
+        const int cg = (int)(h >> 24);
+        const uint32_t tb = ((uint32_t)(4 * (cb + t) + z - nw) & 0xFFu) << 8;
+        hits[cg >= 1 ? p : dump] = (uint16_t)(tb | (h & 0xFFu));
+        hits[cg >= 2 ? p + 1 : dump] = (uint16_t)(tb | ((h >> 8) & 0xFFu));
+        hits[cg == 3 ? p + 2 : dump] = (uint16_t)(tb | ((h >> 16) & 0xFFu));
+        many |= cg >= 4;
+        p += cg;
+      }
+    if (__builtin_expect(__any(many), 0)) {  // types with 4+ columns in this block
+      int pp = start;
+#pragma unroll
+      for (int t = 0; t < MAXQ; ++t)
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          const int cg = (int)(hv[t][z] >> 24);
+          const int e = (int)((hv[t][z] >> 16) & 0xFFu);  // start in csort when cg >= 4
+          const uint32_t tb = ((uint32_t)(4 * (cb + t) + z - nw) & 0xFFu) << 8;
+          if (cg >= 4)
+            for (int x = 2; x < cg; ++x) hits[pp + x] = (uint16_t)(tb | csort[e + x]);
+          pp += cg;
+        }
+    }
+    // -- the 8 rows' lists into the tile record (VGPRs s0/4 and s0/4 + 1) ------
+    // (the wave's LDS accesses are in order: the reads below see the writes)
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int H = 0; H < 2; ++H) {
+        const int rl = 4 * qq + 2 * Lh + H;  // local row of this lane's half
+        const int o0 = off_l[rl];
+        const int cr = (s0 + rl < n) ? (int)off_l[rl + 1] - o0 : 0;
+        uint32_t e = 256u + (uint32_t)x31;  // unused entry: the lane's dump slot
+        if (cr > 32 && x31 == 31)
+          e = (256u + 31u) | (SP2_MARK << 9);
+        else if (x31 < cr)
+          e = tile_entry(hits[o0 + x31]);
+        w |= e << (16 * H);
+      }
+      rtile[tile_word((s0 >> 2) + qq, lane)] = w;
+    }
+    // rows with more than 32 hits: entries 31.. to the overflow list
+#pragma unroll 1
+    for (int rl = 0; rl < RPS && s0 + rl < n; ++rl) {
+      const int o0 = off_l[rl];
+      const int cr = (int)off_l[rl + 1] - o0;
+      if (cr > 32) {
+        const int extra = cr - 31;
+        if (obase + extra > a.cap) {  // a.cap <= SP2_OVF_CAP (tests lower it)
+          fits = false;
+          break;
+        }
+        for (int x = lane; x < extra; x += WAVE) rovf[obase + x] = (uint16_t)tile_entry(hits[o0 + 31 + x]);
+        if (lane == 0) rovfr[s0 + rl] = (uint32_t)obase | ((uint32_t)extra << 16);
+        obase += extra;
+      }
+    }
+  }
+  if (!fits) {  // does not fit: leave the block to the fallback kernel
+    if (lane == 0) {
+      *status = 1;
+      const int p = atomicAdd(a.ovf_cnt, 1);
+      a.ovf_list[p] = b;
+    }
+    return;
+  }
+  ((uint32_t *)(rec + SP2_REC_OWN))[lane] = ((uint32_t *)own)[lane];
+  if (lane == 0) *status = 0;
+}
+
+struct Sp2Lds {
+  size_t ctype, own, ovfr, ovf, u, rem, vrow, rowc, total;
+};
+
+__host__ __device__ __forceinline__ Sp2Lds sp2_lds_layout() {
+  Sp2Lds L;
+  size_t o = 0;
+  L.ctype = o;  o += 256 * 2;                  // column gift types (old)
+  L.own = o;    o += 256;                      // code(i, i): row i's own (old) gift
+  L.ovfr = o;   o += 256 * 4;                  // overflow range per row
+  L.ovf = o;    o += (size_t)SP2_OVF_CAP * 2;  // overflow entries
+  L.u = o;      o += 256 * 8;                  // row duals
+  L.rem = o;    o += 256;                      // scipy's `remaining`: column at position p
+  L.vrow = o;   o += 256;                      // rows reached in the current Dijkstra
+  L.rowc = o;   o += (256 + 32) * 8;           // current row: C[i][j] per column + dump slots
+  L.total = o;
+  return L;
+}
+
+// T[q] for a wave-uniform q (one indexed VGPR move)
+__device__ __forceinline__ uint32_t tile2_get(const u32x32 &T0, const u32x32 &T1, int q) {
+  return (q < 32) ? T0[q] : T1[q - 32];
+}
+
+__global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const unsigned char *rec_all) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int n = a.n;
+  const unsigned char *rec = rec_all + (size_t)b * SP2_REC;
+  if (*(const volatile int32_t *)(rec + SP2_REC_STATUS)) return;  // skipped / left to the fallback
+  const Sp2Lds L = sp2_lds_layout();
+  int16_t *ctype = (int16_t *)(smem + L.ctype);
+  uint8_t *own = smem + L.own;
+  uint32_t *ovfr = (uint32_t *)(smem + L.ovfr);
+  uint16_t *ovf = (uint16_t *)(smem + L.ovf);
+  int64_t *u_l = (int64_t *)(smem + L.u);
+  uint8_t *rem = smem + L.rem;
+  uint8_t *vrow = smem + L.vrow;
+  uint64_t *rowc = (uint64_t *)(smem + L.rowc);
+  const int x31 = lane & 31, Lh = lane >> 5;
+
+  // -- the tile into VGPRs (16 coalesced 16-byte loads per lane), the rest to LDS
+  u32x32 T0, T1;
+  {
+    const uint4 *src = (const uint4 *)(rec + SP2_REC_TILE);
+    const int nq4 = (n + 15) >> 4;  // 16-byte words holding the block's rows
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const uint4 v0 = (w < nq4) ? src[w * 64 + lane] : make_uint4(0, 0, 0, 0);
+      const uint4 v1 = (w + 8 < nq4) ? src[(w + 8) * 64 + lane] : make_uint4(0, 0, 0, 0);
+      T0[4 * w + 0] = v0.x; T0[4 * w + 1] = v0.y; T0[4 * w + 2] = v0.z; T0[4 * w + 3] = v0.w;
+      T1[4 * w + 0] = v1.x; T1[4 * w + 1] = v1.y; T1[4 * w + 2] = v1.z; T1[4 * w + 3] = v1.w;
+    }
+    const uint32_t *ro = (const uint32_t *)(rec + SP2_REC_OVF);
+    for (int x = lane; x < SP2_OVF_CAP / 2; x += WAVE) ((uint32_t *)ovf)[x] = ro[x];
+    const uint32_t *rr = (const uint32_t *)(rec + SP2_REC_OVFR);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ovfr[4 * lane + k] = rr[4 * lane + k];
+    ((uint32_t *)own)[lane] = ((const uint32_t *)(rec + SP2_REC_OWN))[lane];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = 4 * lane + k;
+      if (r < n) ctype[r] = a.types[a.rows[(size_t)b * n + r]];
+    }
+  }
+  for (int r = lane; r < n; r += WAVE) u_l[r] = 0;
+  const int nw1 = a.n_wish + 1;
+  const int64_t E = a.E;
+  const u64x2 E2 = {(uint64_t)E, (uint64_t)E};
+  *(u64x2 *)(rowc + 4 * lane) = E2;
+  *(u64x2 *)(rowc + 4 * lane + 2) = E2;
+  __syncthreads();
+  const uint64_t m1 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
+
+  // -- solve (santa_sp_kernel's step; the row's hits come from the tile) -----------
+  const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
+  const uint64_t BIAS = (uint64_t)KEY_BIAS;
+  int64_t sb[4], W[4];  // spc + BIAS; -v   (columns 4*lane + k)
+  i32x4 path, r4c;
+  uint32_t c4r = ~0u;   // column of row 4*lane + k in byte k (0xFF: none yet)
+  uint32_t lo[4];
+  uint64_t LM[4];       // live (remaining) columns, wave masks
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    W[k] = 0;
+    path[k] = -1;
+    r4c[k] = -1;
+  }
+  uint32_t rem0 = 0;  // rem[p] = n - 1 - p for this lane's 4 positions
+#pragma unroll
+  for (int k = 0; k < 4; ++k) rem0 |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
+  int steps = 0;
+  int fallbacks = 0;
+  if (a.flags & SH_FLAG_BUILD_ONLY) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r4c[k] = 4 * lane + k;
+    c4r = (uint32_t)(4 * lane) * 0x01010101u + 0x03020100u;
+  } else {
+    for (int cur = 0; cur < n; ++cur) {
+      // Dijkstra set-up: remaining = [n-1 .. 0], all columns live.  (The lane
+      // id goes through an empty asm so that the per-column constants below
+      // are recomputed here rather than kept live, or spilled, across the loop.)
+      int ln = lane;
+      int64_t smax = INT64_MAX;  // (from SGPRs: no VGPR pair kept for the constant)
+      asm volatile("" : "+v"(ln), "+s"(smax));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int j = 4 * ln + k;
+        const int pos = n - 1 - j;
+        sb[k] = smax;
+        lo[k] = (r4c[k] < 0) ? (((uint32_t)(1023 - pos) << 10) | (uint32_t)j)
+                             : ((1u << 20) | ((uint32_t)pos << 10) | (uint32_t)r4c[k]);
+        LM[k] = __builtin_amdgcn_ballot_w64(j < n);
+      }
+      ((uint32_t *)rem)[lane] = rem0;
+      if (lane == 0) vrow[0] = (uint8_t)cur;
+      int nvis = 1;
+      int nrem = n;
+      int64_t minVal = 0;
+      int i = cur;
+      int sink;
+      uint32_t kglo = ~0u;        // deferred: key bits of the previous winner
+      uint32_t kX = 0;            // deferred: position-key flip of the moved column
+      int kmover = -1;            //           ... and that column
+      for (;;) {
+        ++steps;
+        // row i: its tile entry (one indexed VGPR move), dual u[i] (LDS broadcast)
+        const uint32_t tw = tile2_get(T0, T1, i >> 2);
+        const uint64_t uraw = (uint64_t)u_l[i];
+        const int mover_v = rem[nrem - 1];  // the column at the last position
+        const uint32_t e = (tw >> ((i & 1) << 4)) & 0xFFFFu;
+        const bool mine = Lh == ((i >> 1) & 1);
+        const uint32_t ea = e >> 9;
+        // previous step's book-keeping (no LDS dependence)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) LM[k] &= ~__builtin_amdgcn_ballot_w64(lo[k] == kglo);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lo[k] ^= (4 * lane + k == kmover) ? kX : 0u;
+        // expand the row: hit columns get -a << 32, the rest stay E
+        rowc[mine ? (int)(e & 0x1FFu) : 256 + x31] = (uint64_t)(uint32_t)(-(int)ea) << 32;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(mine && ea == SP2_MARK) != 0, 0)) {
+          const uint32_t rg = ovfr[i];  // more than 32 hits: the rest from the overflow area
+          const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
+          for (int x = lane; x < oc; x += WAVE) {
+            const uint32_t e2 = ovf[os + x];
+            rowc[e2 & 0x1FFu] = (uint64_t)(uint32_t)(-(int)(e2 >> 9)) << 32;
+          }
+        }
+        const u64x2 c01 = *(const u64x2 *)(rowc + 2 * lane);
+        const u64x2 c23 = *(const u64x2 *)(rowc + 128 + 2 * lane);
+        *(u64x2 *)(rowc + 2 * lane) = E2;
+        *(u64x2 *)(rowc + 128 + 2 * lane) = E2;
+        const uint64_t cc[4] = {c01[0], c01[1], c23[0], c23[1]};
+        // u~[i] = u[i] - (minVal at which row i was reached) = u[i] - minVal now
+        const int64_t ui = (int64_t)rfl_u64(uraw) - minVal;
+        *(lane == 0 ? (int64_t *)&u_l[i] : (int64_t *)&rowc[256 + x31]) = ui;  // lane 0
+        // r + BIAS = C[i][j] - u~[i] - v[j] + BIAS
+        uint64_t bse = BIAS - (uint64_t)ui;
+        asm volatile("" : "+s"(bse));  // keep (W + C) + bse one 64-bit add
+        uint64_t best = ~0ull;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint64_t r = ((uint64_t)W[k] + cc[k]) + bse;
+          const bool lv = __builtin_amdgcn_inverse_ballot_w64(LM[k]);
+          // (a removed column never improves: r >= minVal >= its spc by dual
+          // feasibility, so `upd` needs no live mask)
+          const bool upd = (int64_t)r < sb[k];
+          sb[k] = upd ? (int64_t)r : sb[k];
+          path[k] = upd ? i : path[k];
+          const uint32_t sh = (uint32_t)((uint64_t)sb[k] >> 32), sl = (uint32_t)sb[k];
+          // bits 11..42 of sb (sb > 0 here: spc >= min C - v >= -n_wish * 2^32
+          // > -BIAS); from sb >= 2047 * 2^32 the key saturates at >= 0xFFE00000
+          // and a saturated winner is re-decided by the exact argmin below
+          const uint32_t kh = __builtin_amdgcn_alignbit(min(sh, 2047u), sl, 11);
+          const uint64_t key = ((uint64_t)kh << 32) | ((sl << 21) | lo[k]);
+          best = (lv && key < best) ? key : best;
+        }
+        uint64_t g = rfl_u64(wave_min_u64_fast(best));
+        const uint32_t ghi = (uint32_t)(g >> 32);
+        if (exact || ghi - 1u >= 0xFFDFFFFFu) {  // saturated key (0, or >= 0xFFE00000)
+          // exact two-pass argmin: min sb (signed), then min tie-break bits
+          uint64_t m = ~0ull;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (__builtin_amdgcn_inverse_ballot_w64(LM[k])) m = umin64(m, (uint64_t)sb[k] ^ SIGN64);
+          m = wave_min_u64_dpp(m);
+          const int64_t ms = (int64_t)(m ^ SIGN64);
+          uint64_t b2 = ~0ull;
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (__builtin_amdgcn_inverse_ballot_w64(LM[k]) && sb[k] == ms) b2 = umin64(b2, (uint64_t)lo[k]);
+          g = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wave_min_u64_dpp(b2));
+          minVal = (int64_t)((uint64_t)ms - BIAS);
+          ++fallbacks;
+        } else {
+          minVal = (int64_t)((g >> KEY_LO_BITS) - BIAS);
+        }
+        const uint32_t glo = (uint32_t)g & 0x1FFFFFu;
+        const bool assigned = (glo >> 20) & 1u;
+        const int pk = (int)((glo >> 10) & 1023u);
+        const int aux = (int)(glo & 1023u);
+        const int pstar = assigned ? pk : 1023 - pk;
+        const int last = nrem - 1;
+        // the winner leaves `remaining`; the column at `last` moves to pstar
+        // (applied to the registers at the top of the next step)
+        const int mover = __builtin_amdgcn_readfirstlane(mover_v);
+        kglo = glo;
+        kX = (uint32_t)(last ^ pstar) << 10;
+        kmover = mover;
+        // one store: lane 0 rem[pstar] = mover (a no-op when pstar == last),
+        // lane 1 vrow[nvis] = aux (read only when the winner was assigned)
+        *(lane == 0 ? rem + pstar : lane == 1 ? vrow + nvis : (uint8_t *)&rowc[256] + lane) =
+            (uint8_t)(lane == 0 ? mover : aux);
+        --nrem;
+        if (!assigned) {
+          sink = aux;
+          break;
+        }
+        i = aux;
+        ++nvis;
+      }
+      // (the pending removal of the sink needs no dual update: spc = minVal)
+      // visited rows: u[i] = u~[i] + minVal (= u[i] + minVal - spc[col4row[i]]);
+      // the first 64 are read now and written back after the augmentation
+      const int r0 = vrow[lane];          // stale (but < 256) beyond nvis
+      // visited columns: v[j] -= minVal - spc[j]
+      const uint64_t mvb = (uint64_t)minVal + BIAS;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t vis = ~LM[k] & __builtin_amdgcn_ballot_w64(4 * lane + k < n);
+        const int64_t d = (int64_t)(mvb - (uint64_t)sb[k]);
+        W[k] = __builtin_amdgcn_inverse_ballot_w64(vis) ? W[k] + d : W[k];
+      }
+      const int64_t u0 = u_l[r0];
+      // augment along path[] from the sink back to cur (registers only)
+      int j = sink;
+      for (;;) {
+        const int jl = j >> 2;
+        const int p0 = __builtin_amdgcn_readlane(path[0], jl), p1 = __builtin_amdgcn_readlane(path[1], jl);
+        const int p2 = __builtin_amdgcn_readlane(path[2], jl), p3 = __builtin_amdgcn_readlane(path[3], jl);
+        const int pi = (j & 2) ? ((j & 1) ? p3 : p2) : ((j & 1) ? p1 : p0);
+        // row pi: its previous column t leaves, j becomes its column (scalar
+        // read-modify-write of the packed byte, one writelane)
+        const int pl = pi >> 2, ps = 8 * (pi & 3);
+        const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)c4r, pl);
+        const int t = (int)((cw >> ps) & 0xFFu);
+        const uint32_t nw4 = (cw & ~(0xFFu << ps)) | ((uint32_t)j << ps);
+        // (v_writelane with the lane select in M0: one SGPR operand per VOP3 on
+        // gfx950; the "{m0}" constraint makes the compiler load M0 itself)
+        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(c4r) : "s"(nw4), "{m0}"(pl));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r4c[k] = (4 * lane + k == j) ? pi : r4c[k];
+        j = t;
+        if (pi == cur) break;
+      }
+      if (lane < nvis) u_l[r0] = u0 + minVal;
+      for (int q = lane + WAVE; q < nvis; q += WAVE) {
+        const int r = vrow[q];
+        u_l[r] = u_l[r] + minVal;
+      }
+    }
+  }
+  __syncthreads();
+
+  const uint64_t m2 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
+  // -- outputs: lane handles rows i = 4*lane + k ------------------------------------
+  int64_t cost = 0, dch = 0, dgh = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = 4 * lane + k;
+    const int col = (int)((c4r >> (8 * k)) & 0xFFu);
+    int64_t vq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vq[q] = __shfl(-W[q], col >> 2, WAVE);
+    const int cs = col & 3;
+    const int64_t vcol = (cs == 0) ? vq[0] : (cs == 1) ? vq[1] : (cs == 2) ? vq[2] : vq[3];
+    if (i < n) {
+      const uint32_t co = own[i];
+      const int chd = a.rows[(size_t)b * n + i];
+      const int told = ctype[i], tnew = ctype[col];
+      if (a.flags & SH_FLAG_BUILD_ONLY) {
+        cost += single_cost(co, nw1, E);
+      } else {
+        const int64_t cij = u_l[i] + vcol;  // = C[i][col] (tight matched edge)
+        const uint32_t cn = (cij == E) ? 0u : (uint32_t)((cij >> 32) + nw1);
+        cost += cij;
+        dch += child_happy(cn, nw1) - child_happy(co, nw1);
+        if (a.delta) dgh += gift_happy(a, chd, tnew) - gift_happy(a, chd, told);
+      }
+      if (a.col) a.col[(size_t)b * n + i] = col;
+      a.types[chd] = (int16_t)tnew;  // this block owns chd; ctype holds old types
+    }
+  }
+  cost = wave_sum_i64(cost);
+  dch = wave_sum_i64(dch);
+  dgh = wave_sum_i64(dgh);
+  if (lane == 0) {
+    if (a.cost) a.cost[b] = cost;
+    if (a.steps) a.steps[b] = steps;
+    if ((a.flags & SH_FLAG_TIMING) && a.col && n > 1)  // solve, shader cycles
+      a.col[(size_t)b * n + 1] = (int32_t)min(m2 - m1, (uint64_t)INT32_MAX);
+    if (a.delta) {
+      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
+      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
+    }
+    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Large-block Santa kernel (256 < n <= 4096, both modes): the reference's own
 // block sizes (2000 singles, mpi_single.py:238; 3000 pairs, mpi_twins.py:244).
 //
@@ -2800,6 +3433,9 @@ struct sh_ctx {
   int sp_budget = 0;
   int32_t *d_ovf = nullptr;
   int ovf_cap = 0;
+  // register-tile sparse design: per-block tile records [rec_cap x SP2_REC]
+  unsigned char *d_rec = nullptr;
+  int rec_cap = 0;
   int ovf_par = 0;
   int n_cu = 0;          // compute units (LDS-tile slot count)
   int lds_slots = 0, lds_slots_n = -1;  // cached lds_tile_slots for one n
@@ -2924,6 +3560,7 @@ void sh_ctx_destroy(sh_ctx *ctx) {
   if (ctx->d_csr) (void)hipFree(ctx->d_csr);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   if (ctx->d_ovf) (void)hipFree(ctx->d_ovf);
+  if (ctx->d_rec) (void)hipFree(ctx->d_rec);
   delete ctx;
 }
 
@@ -3020,10 +3657,18 @@ int launch_santa_big(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s
 // Sparse-tile kernel + the fallback launch for blocks whose hit lists did not
 // fit.  The two overflow counters alternate between calls: the fallback
 // launch of call k resets the counter that call k+1 appends to.
-int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
+int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) {
   const int cap = sp_capacity(ctx);
-  const SpLds L = sp_lds_layout(ctx->ng, cap);
-  if (L.total > 64 * 1024) return fail(SH_ERR_ARGS, "sparse-tile LDS budget above 64 KiB");
+  const size_t lds = tile2 ? tile_lds_layout(ctx->ng).total : sp_lds_layout(ctx->ng, cap).total;
+  if (lds > 64 * 1024) return fail(SH_ERR_ARGS, "sparse-tile LDS budget above 64 KiB");
+  if (tile2 && ctx->rec_cap < B) {  // per-block tile records (HBM)
+    if (ctx->d_rec) HIP_TRY(hipFree(ctx->d_rec));
+    ctx->d_rec = nullptr;
+    ctx->rec_cap = 0;
+    const int capB = std::max(B, 4096);
+    HIP_TRY(hipMalloc(&ctx->d_rec, (size_t)capB * SP2_REC));
+    ctx->rec_cap = capB;
+  }
   if (ctx->ovf_cap < B) {
     if (ctx->d_ovf) HIP_TRY(hipFree(ctx->d_ovf));
     ctx->d_ovf = nullptr;
@@ -3039,10 +3684,22 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   a.ovf_cnt = ctx->d_ovf + p;
   a.ovf_list = ctx->d_ovf + 2 + (size_t)p * ctx->ovf_cap;
   a.blist = nullptr;
-  if (ctx->n_wish % 4 == 0)
-    hipLaunchKernelGGL(santa_sp_kernel<true>, dim3(B), dim3(WAVE), L.total, s, a);
+  const bool vec = ctx->n_wish % 4 == 0;
+  if (tile2) {
+    // overflow capacity per block; a sparse budget set for tests lowers it
+    // (budget / 16 entries) so that some or all blocks take the fallback
+    a.cap = ctx->sp_budget > 0 ? std::min(SP2_OVF_CAP, ctx->sp_budget / 16) : SP2_OVF_CAP;
+    if (vec)
+      hipLaunchKernelGGL(santa_tile_kernel<true>, dim3(B), dim3(WAVE), lds, s, a, ctx->d_rec);
+    else
+      hipLaunchKernelGGL(santa_tile_kernel<false>, dim3(B), dim3(WAVE), lds, s, a, ctx->d_rec);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(santa_sp2_kernel, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
+                       (const unsigned char *)ctx->d_rec);
+  } else if (vec)
+    hipLaunchKernelGGL(santa_sp_kernel<true>, dim3(B), dim3(WAVE), lds, s, a);
   else
-    hipLaunchKernelGGL(santa_sp_kernel<false>, dim3(B), dim3(WAVE), L.total, s, a);
+    hipLaunchKernelGGL(santa_sp_kernel<false>, dim3(B), dim3(WAVE), lds, s, a);
   HIP_TRY(hipGetLastError());
   SantaArgs f = a;
   f.blist = a.ovf_list;
@@ -3089,13 +3746,16 @@ int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   // the sparse kernel packs child ids (< 2^20) and gift types (< 1023) in one
   // dword during its build; other instances take the register-tile kernel
   if ((flags & SH_FLAG_VT_TILE) || ctx->nc > (1 << 20) || ctx->ng > 1022) return SH_DESIGN_VT_TILE;
-  if (flags & SH_FLAG_SP_TILE) return SH_DESIGN_SPARSE;
+  // the register-tile sparse kernel keeps the wish value in 7 bits with one
+  // code reserved (n_wish <= 126); the LDS-list kernel takes the rest
+  const int sparse = (ctx->n_wish <= 126 && !(flags & SH_FLAG_SP1)) ? SH_DESIGN_SPARSE2 : SH_DESIGN_SPARSE;
+  if (flags & (SH_FLAG_SP_TILE | SH_FLAG_SP1)) return sparse;
   // few blocks (at most one resident wave of LDS-tile blocks): every block
   // starts at once and the launch takes one block's latency, which the
   // 4-wave tile kernel has lower (MI355X, one GPU's shard of a round at 8
   // GPUs, 466 blocks: 2.25 vs 2.41 ms at round 0, 0.81 vs 0.95 ms at round 10)
   if (B <= lds_tile_slots(ctx, n)) return SH_DESIGN_LDS_TILE;
-  return SH_DESIGN_SPARSE;
+  return sparse;
 }
 
 // Blocks of kernel f the device holds at once (occupancy API x CUs).
@@ -3129,6 +3789,7 @@ int resident_blocks(sh_ctx *ctx, int design, int mode, int n) {
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
     case SH_DESIGN_SW_TILE: return occ_blocks(ctx, santa_sw_kernel, WAVE, sw_lds_layout(ctx->ng).total);
     case SH_DESIGN_VT_TILE: return occ_blocks(ctx, santa_vt_kernel<0>, VT_WG, vt_lds_layout(ctx->ng).total);
+    case SH_DESIGN_SPARSE2: return occ_blocks(ctx, santa_sp2_kernel, WAVE, sp2_lds_layout().total);
     default:
       return occ_blocks(ctx, santa_sp_kernel<true>, WAVE, sp_lds_layout(ctx->ng, sp_capacity(ctx)).total);
   }
@@ -3162,7 +3823,8 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
     case SH_DESIGN_LDS_TILE: return launch_santa<1, 0>(ctx, a, B, s);
     case SH_DESIGN_SW_TILE: return launch_santa_sw(ctx, a, B, s);
     case SH_DESIGN_VT_TILE: return launch_santa_vt<0>(ctx, a, B, s);
-    default: return launch_santa_sp(ctx, a, B, s);
+    case SH_DESIGN_SPARSE2: return launch_santa_sp(ctx, a, B, s, true);
+    default: return launch_santa_sp(ctx, a, B, s, false);
   }
 }
 

@@ -26,13 +26,15 @@ SH_FLAG_SW_TILE = 16
 SH_FLAG_VT_TILE = 32
 SH_FLAG_TIMING = 64
 SH_FLAG_SP_TILE = 128
+SH_FLAG_SP1 = 256
 SH_ERRF_ROWS = 1
 SH_ERRF_INFEASIBLE = 2
 SH_ERRF_TYPE = 4
 SH_DESIGN_NAMES = {0: "santa_sp_kernel (1-wave sparse LDS tile)", 1: "santa_block_kernel (4-wave LDS byte tile)",
                    2: "santa_sw_kernel (1-wave register tile)", 3: "santa_vt_kernel (4-wave register tile)",
                    4: "santa_block_kernel (twins, 4-wave code-pair tile)",
-                   5: "santa_big_kernel (row rebuilt from the wishlist)"}
+                   5: "santa_big_kernel (row rebuilt from the wishlist)",
+                   6: "santa_sp2_kernel (1-wave sparse register tile)"}
 SH_MAX_N = 1024
 SH_MAX_N_SANTA = 4096
 

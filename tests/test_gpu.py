@@ -148,7 +148,7 @@ def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
     s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
     # singles n <= 256: the default for few blocks (LDS tile) and the forced
     # throughput kernel (sparse) are both checked
-    for fl in ((0, _lib.SH_FLAG_SP_TILE) if mode == 0 and n <= 256 else (0,)):
+    for fl in ((0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1) if mode == 0 and n <= 256 else (0,)):
         types = ctx.upload_types(full_data.types)
         col = torch.empty(B * n, dtype=torch.int32, device="cuda")
         cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -387,20 +387,25 @@ def _round_outputs(ctx, full_data, mode, rows, nn, B, fl=0):
     return [x.cpu().numpy() for x in (col, cost, delta, steps, types)]
 
 
-def test_sparse_overflow_fallback(sh, ctx, full_data):
-    """Blocks whose hit lists do not fit the sparse kernel's LDS budget are
-    solved by the register-tile fallback launch; any budget gives the same
-    round (all blocks overflowing, some, none), repeated calls included
-    (the double-buffered overflow counters)."""
+@pytest.mark.parametrize("design", ["tile2", "sp1"])
+def test_sparse_overflow_fallback(sh, ctx, full_data, design):
+    """Blocks that do not fit the sparse kernels' on-chip capacity (sp1: the
+    LDS hit-list budget; tile2: the overflow list of rows with more than 32
+    hits, capacity budget / 16 entries) are solved by the register-tile
+    fallback launch; any budget gives the same round (all blocks
+    overflowing, some, none), repeated calls included (the double-buffered
+    overflow counters)."""
     from santa_hip import _lib
     B, nn = 96, 256
     rows = ctx.sample_blocks(0, nn, B, 5, 3)
     want = _round_outputs(ctx, full_data, 0, rows, nn, B, _lib.SH_FLAG_VT_TILE)
+    fl = _lib.SH_FLAG_SP_TILE if design == "tile2" else _lib.SH_FLAG_SP1
+    budgets = (16, 1600, 2400, 0, 0, 800, 0) if design == "tile2" else (6000, 16500, 17500, 0, 0, 4096, 0)
     try:
-        for budget in (6000, 16500, 17500, 0, 0, 4096, 0):
+        for budget in budgets:
             cap = ctx.set_sparse_budget(budget)
             assert cap >= 0
-            got = _round_outputs(ctx, full_data, 0, rows, nn, B, _lib.SH_FLAG_SP_TILE)
+            got = _round_outputs(ctx, full_data, 0, rows, nn, B, fl)
             for x, y in zip(want, got):
                 assert np.array_equal(x, y), budget
         assert ctx.error_flags() == 0
@@ -418,8 +423,8 @@ def test_kernel_designs_agree(sh, ctx, full_data):
     for B, nn in ((64, 256), (16, 100), (8, 37), (8, 130), (4, 1), (6, 255), (5, 64)):
         rows = ctx.sample_blocks(mode, nn, B, 77, 9)
         outs = []
-        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_SW_TILE,
-                   _lib.SH_FLAG_LDS_TILE):
+        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_SP1, _lib.SH_FLAG_VT_TILE,
+                   _lib.SH_FLAG_SW_TILE, _lib.SH_FLAG_LDS_TILE):
             types = ctx.upload_types(full_data.types)
             col = torch.empty(B * nn, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -439,10 +444,13 @@ def test_design_dispatch(sh, ctx):
     blocks (one GPU's shard at 8 GPUs: 466), the sparse kernel again when
     forced; twins and large blocks have one design each."""
     from santa_hip import _lib
-    assert ctx.solve_design(0, 256, 3730) == 0
+    assert ctx.solve_design(0, 256, 3730) == 6
     assert ctx.solve_design(0, 256, 466) == 1
-    assert ctx.solve_design(0, 256, 466, _lib.SH_FLAG_SP_TILE) == 0
-    assert ctx.solve_design(0, 256, 933) == 0
+    assert ctx.solve_design(0, 256, 466, _lib.SH_FLAG_SP_TILE) == 6
+    assert ctx.solve_design(0, 256, 3730, _lib.SH_FLAG_SP1) == 0
+    assert ctx.solve_design(0, 256, 933) == 6
+    # the register-tile design holds a whole round at once (4 waves per SIMD)
+    assert ctx.resident_blocks(0, 256, 3730) >= 3730
     assert ctx.solve_design(1, 256, 78) == 4
     assert ctx.solve_design(0, 2000, 477) == 5
     assert ctx.solve_design(1, 3000, 6) == 5
@@ -519,7 +527,7 @@ def test_santa_edge_block_sizes_vs_oracle(sh, ctx, full_data, mode, n, B):
                                       ng=full_data.ng)
     s0 = oracle.score_sums(full_data.wish, full_data.goodkids, full_data.types)
     s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
-    for fl in ((0, _lib.SH_FLAG_SP_TILE) if mode == 0 else (0,)):
+    for fl in ((0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1) if mode == 0 else (0,)):
         types = ctx.upload_types(full_data.types)
         col = torch.empty(B * n, dtype=torch.int32, device="cuda")
         cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -590,7 +598,7 @@ def test_bench_launches_n_ranks(sh):
 
 
 # --------------------------------------------------------------------------- input validation
-@pytest.mark.parametrize("mode,n,fl", [(0, 256, 128), (0, 256, 8), (0, 256, 32), (0, 256, 16),
+@pytest.mark.parametrize("mode,n,fl", [(0, 256, 128), (0, 256, 256), (0, 256, 8), (0, 256, 32), (0, 256, 16),
                                        (1, 256, 0), (0, 300, 0), (1, 300, 0)])
 def test_gift_type_out_of_range_is_flagged_not_used(sh, ctx, full_data, mode, n, fl):
     """A current gift type outside [0, ng) in a block (it would index the
