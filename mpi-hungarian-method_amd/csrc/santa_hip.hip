@@ -305,29 +305,26 @@ __device__ __forceinline__ uint64_t wave_min_u64_dpp(uint64_t x) {
   return readlane_u64(x, 63);
 }
 
-// 32-bit unsigned min over the wave with the DPP modifier fused into
-// v_min_u32 (one instruction per level); the result is read from lane 63.
-// Hazards are explicit: a VALU write followed by a DPP read of the same VGPR
-// needs two wait states (s_nop 1) on GFX9.
+// 32-bit unsigned min over the wave, one DPP level at a time (quad perms,
+// half-row/row mirrors, row_bcast15/31); the result is read from lane 63.
+// Written with builtins (old value ~0, the identity of min) so that the
+// compiler fuses each level into one v_min_u32_dpp, inserts only the hazard
+// wait states it needs and may fill them with independent work of the step
+// (an asm block with explicit s_nop 1 pads cost 8 cycles per level:
+// tools/calib/step_lat.hip).
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp_min_step(uint32_t x) {
+  const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, CTRL, ROWMASK, 0xF, false);
+  return y < x ? y : x;
+}
 __device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t x) {
-  uint32_t r;
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_min_u32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_min_u32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_min_u32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_min_u32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_min_u32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_min_u32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
-      "s_nop 1\n\t"
-      "v_readlane_b32 %1, %0, 63"
-      : "+v"(x), "=s"(r));
-  return r;
+  x = dpp_min_step<0xB1, 0xF>(x);   // quad_perm [1,0,3,2]
+  x = dpp_min_step<0x4E, 0xF>(x);   // quad_perm [2,3,0,1]
+  x = dpp_min_step<0x141, 0xF>(x);  // row_half_mirror
+  x = dpp_min_step<0x140, 0xF>(x);  // row_mirror
+  x = dpp_min_step<0x142, 0xA>(x);  // row_bcast:15 -> rows 1, 3
+  x = dpp_min_step<0x143, 0xC>(x);  // row_bcast:31 -> rows 2, 3
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
 // 64-bit unsigned min as two fused 32-bit reductions (high word, then the
@@ -2597,7 +2594,7 @@ __global__ __launch_bounds__(WAVE) void santa_tile_kernel(SantaArgs a, unsigned 
 }
 
 struct Sp2Lds {
-  size_t ctype, own, ovfr, ovf, u, rem, vrow, rowc, total;
+  size_t ctype, own, ovfr, ovf, u, rem, rowc, total;
 };
 
 __host__ __device__ __forceinline__ Sp2Lds sp2_lds_layout() {
@@ -2609,7 +2606,6 @@ __host__ __device__ __forceinline__ Sp2Lds sp2_lds_layout() {
   L.ovf = o;    o += (size_t)SP2_OVF_CAP * 2;  // overflow entries
   L.u = o;      o += 256 * 8;                  // row duals
   L.rem = o;    o += 256;                      // scipy's `remaining`: column at position p
-  L.vrow = o;   o += 256;                      // rows reached in the current Dijkstra
   L.rowc = o;   o += (256 + 32) * 8;           // current row: C[i][j] per column + dump slots
   L.total = o;
   return L;
@@ -2634,7 +2630,6 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
   uint16_t *ovf = (uint16_t *)(smem + L.ovf);
   int64_t *u_l = (int64_t *)(smem + L.u);
   uint8_t *rem = smem + L.rem;
-  uint8_t *vrow = smem + L.vrow;
   uint64_t *rowc = (uint64_t *)(smem + L.rowc);
   const int x31 = lane & 31, Lh = lane >> 5;
 
@@ -2665,9 +2660,11 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
   for (int r = lane; r < n; r += WAVE) u_l[r] = 0;
   const int nw1 = a.n_wish + 1;
   const int64_t E = a.E;
-  const u64x2 E2 = {(uint64_t)E, (uint64_t)E};
-  *(u64x2 *)(rowc + 4 * lane) = E2;
-  *(u64x2 *)(rowc + 4 * lane + 2) = E2;
+  {
+    const u64x2 E2 = {(uint64_t)E, (uint64_t)E};
+    *(u64x2 *)(rowc + 4 * lane) = E2;
+    *(u64x2 *)(rowc + 4 * lane + 2) = E2;
+  }
   __syncthreads();
   const uint64_t m1 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
 
@@ -2712,8 +2709,6 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         LM[k] = __builtin_amdgcn_ballot_w64(j < n);
       }
       ((uint32_t *)rem)[lane] = rem0;
-      if (lane == 0) vrow[0] = (uint8_t)cur;
-      int nvis = 1;
       int nrem = n;
       int64_t minVal = 0;
       int i = cur;
@@ -2723,7 +2718,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
       int kmover = -1;            //           ... and that column
       for (;;) {
         ++steps;
-        // row i: its tile entry (one indexed VGPR move), dual u[i] (LDS broadcast)
+        // row i: its tile entry (one indexed VGPR move), dual u[i] (LDS broadcast;
+        // u stays unchanged during a Dijkstra: the rows' updates are applied at
+        // its end from the removed columns)
         const uint32_t tw = tile2_get(T0, T1, i >> 2);
         const uint64_t uraw = (uint64_t)u_l[i];
         const int mover_v = rem[nrem - 1];  // the column at the last position
@@ -2735,9 +2732,11 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         for (int k = 0; k < 4; ++k) LM[k] &= ~__builtin_amdgcn_ballot_w64(lo[k] == kglo);
 #pragma unroll
         for (int k = 0; k < 4; ++k) lo[k] ^= (4 * lane + k == kmover) ? kX : 0u;
-        // expand the row: hit columns get -a << 32, the rest stay E
-        rowc[mine ? (int)(e & 0x1FFu) : 256 + x31] = (uint64_t)(uint32_t)(-(int)ea) << 32;
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(mine && ea == SP2_MARK) != 0, 0)) {
+        // expand the row: hit columns get -a << 32, the rest hold E
+        const int sslot = mine ? (int)(e & 0x1FFu) : 256 + x31;
+        rowc[sslot] = (uint64_t)(uint32_t)(-(int)ea) << 32;
+        const bool ovr = __builtin_amdgcn_ballot_w64(mine && ea == SP2_MARK) != 0;
+        if (__builtin_expect(ovr, 0)) {
           const uint32_t rg = ovfr[i];  // more than 32 hits: the rest from the overflow area
           const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
           for (int x = lane; x < oc; x += WAVE) {
@@ -2747,12 +2746,16 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         }
         const u64x2 c01 = *(const u64x2 *)(rowc + 2 * lane);
         const u64x2 c23 = *(const u64x2 *)(rowc + 128 + 2 * lane);
-        *(u64x2 *)(rowc + 2 * lane) = E2;
-        *(u64x2 *)(rowc + 128 + 2 * lane) = E2;
+        // un-scatter: the slots written above get E back (in-order LDS: after the reads)
+        rowc[sslot] = (uint64_t)E;
+        if (__builtin_expect(ovr, 0)) {
+          const uint32_t rg = ovfr[i];
+          const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
+          for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = (uint64_t)E;
+        }
         const uint64_t cc[4] = {c01[0], c01[1], c23[0], c23[1]};
-        // u~[i] = u[i] - (minVal at which row i was reached) = u[i] - minVal now
+        // u~[i] = u[i] - minVal (row i is reached at the current minimum)
         const int64_t ui = (int64_t)rfl_u64(uraw) - minVal;
-        *(lane == 0 ? (int64_t *)&u_l[i] : (int64_t *)&rowc[256 + x31]) = ui;  // lane 0
         // r + BIAS = C[i][j] - u~[i] - v[j] + BIAS
         uint64_t bse = BIAS - (uint64_t)ui;
         asm volatile("" : "+s"(bse));  // keep (W + C) + bse one 64-bit add
@@ -2806,31 +2809,31 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         kglo = glo;
         kX = (uint32_t)(last ^ pstar) << 10;
         kmover = mover;
-        // one store: lane 0 rem[pstar] = mover (a no-op when pstar == last),
-        // lane 1 vrow[nvis] = aux (read only when the winner was assigned)
-        *(lane == 0 ? rem + pstar : lane == 1 ? vrow + nvis : (uint8_t *)&rowc[256] + lane) =
-            (uint8_t)(lane == 0 ? mover : aux);
+        rem[pstar] = (uint8_t)mover;  // (every lane, same byte; a no-op when pstar == last)
         --nrem;
         if (!assigned) {
           sink = aux;
           break;
         }
         i = aux;
-        ++nvis;
       }
-      // (the pending removal of the sink needs no dual update: spc = minVal)
-      // visited rows: u[i] = u~[i] + minVal (= u[i] + minVal - spc[col4row[i]]);
-      // the first 64 are read now and written back after the augmentation
-      const int r0 = vrow[lane];          // stale (but < 256) beyond nvis
-      // visited columns: v[j] -= minVal - spc[j]
+      // Dual update (scipy: u[cur] += minVal; u[i] += minVal - spc[col4row[i]]
+      // for the other visited rows; v[j] -= minVal - spc[j] for the removed
+      // columns).  The visited rows other than cur are the rows of the removed
+      // assigned columns, and a removed column's spc is frozen since its removal
+      // (it never improves again), so the column owners apply both updates;
+      // the matching makes the rows distinct (plain LDS adds, no conflicts).
+      // (The pending removal of the sink needs no update: spc = minVal.)
       const uint64_t mvb = (uint64_t)minVal + BIAS;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint64_t vis = ~LM[k] & __builtin_amdgcn_ballot_w64(4 * lane + k < n);
+        const bool vk = __builtin_amdgcn_inverse_ballot_w64(vis);
         const int64_t d = (int64_t)(mvb - (uint64_t)sb[k]);
-        W[k] = __builtin_amdgcn_inverse_ballot_w64(vis) ? W[k] + d : W[k];
+        W[k] = vk ? W[k] + d : W[k];
+        if (vk && r4c[k] >= 0) u_l[r4c[k]] += d;
       }
-      const int64_t u0 = u_l[r0];
+      if (lane == 0) u_l[cur] += minVal;
       // augment along path[] from the sink back to cur (registers only)
       int j = sink;
       for (;;) {
@@ -2851,11 +2854,6 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         for (int k = 0; k < 4; ++k) r4c[k] = (4 * lane + k == j) ? pi : r4c[k];
         j = t;
         if (pi == cur) break;
-      }
-      if (lane < nvis) u_l[r0] = u0 + minVal;
-      for (int q = lane + WAVE; q < nvis; q += WAVE) {
-        const int r = vrow[q];
-        u_l[r] = u_l[r] + minVal;
       }
     }
   }
