@@ -219,8 +219,16 @@ def scipy_baseline(sd, mode, n, seconds, ncores, rows, lo, count, stride, nb):
 
 
 # --------------------------------------------------------------------------- HBM traffic
-def stored_traffic(kname: str):
-    """HBM bytes per launch of `kname` from the newest committed rocprofv3 PMC
+def design_kernels(kname: str):
+    """The kernels one solve launch of a design runs (the register-tile sparse
+    design builds its tiles in santa_tile_kernel, then solves in santa_sp2_kernel;
+    the events around the solve bracket both)."""
+    k = kname.split(" ")[0].split("<")[0]
+    return ["santa_tile_kernel", k] if k == "santa_sp2_kernel" else [k]
+
+
+def stored_traffic(knames):
+    """HBM bytes per launch of the kernels `knames` (summed) from the newest committed rocprofv3 PMC
     summary taken on THIS kernel source (tools/profile_round.sh ->
     profiles/<tag>_summary.json records the source hash).  FETCH_SIZE is
     scaled by the factor calibrated for this kernel's access pattern (random
@@ -236,11 +244,14 @@ def stored_traffic(kname: str):
             continue
         if s.get("source_sha16") != src:
             continue
-        e = s.get("hbm_bytes_per_launch", {}).get(kname, {})
-        if "FETCH_SIZE_bytes" in e and "WRITE_SIZE_bytes" in e:
+        hb = s.get("hbm_bytes_per_launch", {})
+        es = [hb.get(k, {}) for k in knames]
+        if all("FETCH_SIZE_bytes" in e and "WRITE_SIZE_bytes" in e for e in es):
             k = json.load(open(calib[-1]))["gather_correction_factor"] if calib else 1.0
-            return {"traffic": round(e["FETCH_SIZE_bytes"] * k + e["WRITE_SIZE_bytes"]),
-                    "traffic_raw": {"FETCH_SIZE": e["FETCH_SIZE_bytes"], "WRITE_SIZE": e["WRITE_SIZE_bytes"],
+            fetch = sum(e["FETCH_SIZE_bytes"] for e in es)
+            write = sum(e["WRITE_SIZE_bytes"] for e in es)
+            return {"traffic": round(fetch * k + write),
+                    "traffic_raw": {"FETCH_SIZE": fetch, "WRITE_SIZE": write, "kernels": knames,
                                     "fetch_correction": round(k, 4)},
                     "traffic_source": f"{os.path.basename(path)} (kernel source {src})"}
     return {"traffic": None,
@@ -419,7 +430,7 @@ def main():
         bmax = int(st[0].argmax())
         rows0 = ctx.sample_blocks(mode, n, nb, args.seed, 0)
         one = rows0[(b0 + bmax) * n:(b0 + bmax + 1) * n].contiguous()
-        force = {0: _lib.SH_FLAG_SP_TILE, 1: _lib.SH_FLAG_LDS_TILE}.get(design, 0)
+        force = {0: _lib.SH_FLAG_SP_TILE, 6: _lib.SH_FLAG_SP_TILE, 1: _lib.SH_FLAG_LDS_TILE}.get(design, 0)
         lone = []
         for _ in range(3):
             tt = ctx.upload_types(sd.types)
@@ -487,7 +498,7 @@ def main():
         "cpu": cpu,
     }
     if mode == 0 and world == 1:  # the PMC passes profile a full one-GPU round
-        out["roofline"].update(stored_traffic(kname.split(" ")[0].split("<")[0]))
+        out["roofline"].update(stored_traffic(design_kernels(kname)))
     if want_cpu:
         cb = cpu_baseline(sd, mode, n, args.cpu_seconds, cpu["used"])
         cb["cpu_model"] = cpu["model"]

@@ -2308,8 +2308,10 @@ constexpr size_t SP2_REC_OWN = SP2_REC_OVFR + 256 * 4;
 constexpr size_t SP2_REC_STATUS = SP2_REC_OWN + 256;
 constexpr size_t SP2_REC = SP2_REC_STATUS + 128;  // 18816 bytes
 
+constexpr int TILE_NW = 4;  // waves per block of the tile build (64 rows each)
+
 struct TileLds {
-  size_t own, csort, thead, off, hits, total;
+  size_t own, csort, thead, ocnt, off, hits, total;
 };
 
 __host__ __device__ __forceinline__ TileLds tile_lds_layout(int ng) {
@@ -2318,8 +2320,9 @@ __host__ __device__ __forceinline__ TileLds tile_lds_layout(int ng) {
   L.own = o;    o += 256;                      // code(i, i): row i's own (old) gift
   L.csort = o;  o += 272;                      // columns sorted by gift type (+ pad)
   L.thead = o;  o += r16((size_t)ng * 4);      // counting-sort counters, then the type table
-  L.off = o;    o += 32;                       // hit-list offsets of the sub-round's 8 rows
-  L.hits = o;   o += (SP2_SUB_CAP + 2 * 64) * 2;  // the sub-round's hit list + a dump per lane
+  L.ocnt = o;   o += 16;                       // overflow entries allocated (all waves)
+  L.off = o;    o += TILE_NW * 32;             // per wave: hit-list offsets of its sub-round's 8 rows
+  L.hits = o;   o += TILE_NW * (SP2_SUB_CAP + 2 * 64) * 2;  // per wave: the sub-round's list + dumps
   L.total = o;
   return L;
 }
@@ -2333,66 +2336,58 @@ __device__ __forceinline__ uint32_t tile_entry(uint32_t h) {
   return (h & 0xFFu) | ((uint32_t)(-(int)(int8_t)(h >> 8)) << 9);
 }
 
+// Four waves per block: the column sort is shared, then wave w builds rows
+// 64w..64w+63 (8 sub-rounds of 8 rows) with its own LDS list, so a block's
+// 32 dependent wishlist-load rounds run as 4 chains of 8.  Overflow entries
+// are allocated from one LDS counter (a block fits iff its total overflow
+// does, whatever the order the waves allocate in).
 template <bool VEC>
-__global__ __launch_bounds__(WAVE) void santa_tile_kernel(SantaArgs a, unsigned char *rec_all) {
+__global__ __launch_bounds__(TILE_NW * WAVE) void santa_tile_kernel(SantaArgs a, unsigned char *rec_all) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n = a.n;
   const TileLds L = tile_lds_layout(a.ng);
   uint8_t *own = smem + L.own;
   uint8_t *csort = smem + L.csort;
   uint32_t *thead = (uint32_t *)(smem + L.thead);
   uint32_t *tcnt = thead;  // counting-sort counters, turned into the type table in place
-  uint16_t *off_l = (uint16_t *)(smem + L.off);
-  uint16_t *hits = (uint16_t *)(smem + L.hits);
+  int32_t *ocnt = (int32_t *)(smem + L.ocnt);
+  uint16_t *off_l = (uint16_t *)(smem + L.off) + wv * 16;
+  uint16_t *hits = (uint16_t *)(smem + L.hits) + wv * (SP2_SUB_CAP + 2 * 64);
   unsigned char *rec = rec_all + (size_t)b * SP2_REC;
   uint32_t *rtile = (uint32_t *)(rec + SP2_REC_TILE);
   uint16_t *rovf = (uint16_t *)(rec + SP2_REC_OVF);
   uint32_t *rovfr = (uint32_t *)(rec + SP2_REC_OVFR);
   int32_t *status = (int32_t *)(rec + SP2_REC_STATUS);
 
-  // -- rows (lane l owns rows 4l..4l+3), range check --------------------------------
-  int child[4];
-  int bad = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int r = 4 * lane + k;
-    child[k] = (r < n) ? a.rows[(size_t)b * n + r] : 0;
-    bad |= (r < n) && ((child[k] < 0) || (child[k] >= a.nc));
-  }
-  if (__any(bad)) {
-    if (lane == 0) {
+  // -- rows (thread t owns row t), range check ----------------------------------------
+  const bool live = tid < n;
+  const int child = live ? a.rows[(size_t)b * n + tid] : 0;
+  if (__syncthreads_or(live && (child < 0 || child >= a.nc))) {
+    if (tid == 0) {
       atomicOr(a.err, SH_ERRF_ROWS);
       *status = 1;  // skip
     }
     return;
   }
   // -- columns sorted by gift type (counting sort, as santa_sp_kernel) ---------------
-  for (int t = lane; t < a.ng; t += WAVE) tcnt[t] = 0u;
-  ((uint32_t *)own)[lane] = 0;
-  int myt[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) myt[k] = (4 * lane + k < n) ? a.types[child[k]] : -1;
-  {  // the types index LDS tables: reject the block if one is out of range
-    int badt = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) badt |= (4 * lane + k < n) && (myt[k] < 0 || myt[k] >= a.ng);
-    if (__any(badt)) {
-      if (lane == 0) {
-        atomicOr(a.err, SH_ERRF_TYPE);
-        *status = 1;
-      }
-      return;
+  for (int t = tid; t < a.ng; t += TILE_NW * WAVE) tcnt[t] = 0u;
+  if (tid < 64) ((uint32_t *)own)[tid] = 0;
+  if (tid == 0) *ocnt = 0;
+  const int myt = live ? a.types[child] : -1;
+  // the types index LDS tables: reject the block if one is out of range
+  if (__syncthreads_or(live && (myt < 0 || myt >= a.ng))) {
+    if (tid == 0) {
+      atomicOr(a.err, SH_ERRF_TYPE);
+      *status = 1;
     }
+    return;
   }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (myt[k] >= 0) atomicAdd(&tcnt[myt[k]], 1u << 16);
+  if (myt >= 0) atomicAdd(&tcnt[myt], 1u << 16);
   __syncthreads();
   int big = 0;
-  {  // exclusive scan of the counts over types -> start of each type in csort
+  if (wv == 0) {  // exclusive scan of the counts over types -> start of each type in csort
     const int per = (a.ng + WAVE - 1) / WAVE;
     const int t0s = lane * per, t1s = min(a.ng, t0s + per);
     uint32_t sum = 0;
@@ -2405,22 +2400,23 @@ __global__ __launch_bounds__(WAVE) void santa_tile_kernel(SantaArgs a, unsigned 
       run += h >> 16;
     }
   }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (myt[k] >= 0) csort[atomicAdd(&tcnt[myt[k]], 1u) & 0xFFFFu] = (uint8_t)rowc_slot(4 * lane + k);
-  __syncthreads();
-  {  // per type, in place: c0 | c1 << 8 | (count <= 3 ? c2 : start in csort) << 16 | count << 24
-    const int per = (a.ng + WAVE - 1) / WAVE;
-    const int t0s = lane * per, t1s = min(a.ng, t0s + per);
-    for (int t = t0s; t < t1s; ++t) {
-      const uint32_t h = tcnt[t];
-      const uint32_t c = h >> 16, e = (h & 0xFFFFu) - c;  // start in csort
-      const uint32_t x2 = c <= 3u ? (uint32_t)csort[e + 2] : e;
-      thead[t] = c ? ((uint32_t)csort[e] | ((uint32_t)csort[e + 1] << 8) | (x2 << 16) |
-                      (min(c, 255u) << 24))
-                   : 0u;
+  if (__syncthreads_or(big)) {  // a type with 255+ columns: leave the block to the fallback
+    if (tid == 0) {
+      *status = 1;
+      const int p = atomicAdd(a.ovf_cnt, 1);
+      a.ovf_list[p] = b;
     }
+    return;
+  }
+  if (myt >= 0) csort[atomicAdd(&tcnt[myt], 1u) & 0xFFFFu] = (uint8_t)rowc_slot(tid);
+  __syncthreads();
+  // per type, in place: c0 | c1 << 8 | (count <= 3 ? c2 : start in csort) << 16 | count << 24
+  for (int t = tid; t < a.ng; t += TILE_NW * WAVE) {
+    const uint32_t h = tcnt[t];
+    const uint32_t c = h >> 16, e = (h & 0xFFFFu) - c;  // start in csort
+    const uint32_t x2 = c <= 3u ? (uint32_t)csort[e + 2] : e;
+    thead[t] = c ? ((uint32_t)csort[e] | ((uint32_t)csort[e + 1] << 8) | (x2 << 16) | (min(c, 255u) << 24))
+                 : 0u;
   }
   __syncthreads();
 
@@ -2436,7 +2432,7 @@ __global__ __launch_bounds__(WAVE) void santa_tile_kernel(SantaArgs a, unsigned 
   const int nch = (nw + 3) >> 2;
   const int ncq = (nch + LPR - 1) / LPR;
   const int qr = lane / LPR, qj = lane % LPR;
-  bool fits = !__any(big);
+  bool fits = true;
   auto load_chunk = [&](const int16_t *src, int c) -> uint2 {
     uint2 q;
     if constexpr (VEC) {
@@ -2458,20 +2454,15 @@ __global__ __launch_bounds__(WAVE) void santa_tile_kernel(SantaArgs a, unsigned 
   };
   const int dump = SP2_SUB_CAP + 2 * lane;
   const int cb = qj * ncq;
-  int ct[4];  // child id | (own type + 1) << 20 (children < 2^20, types < 1023)
-#pragma unroll
-  for (int k = 0; k < 4; ++k) ct[k] = child[k] | ((myt[k] + 1) << 20);
-  auto row_child = [&](int row, int &chd, int &mt) {
-    int x = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c2 = __shfl(ct[k], (row >> 2) & 63, WAVE);
-      x = ((row & 3) == k) ? c2 : x;
-    }
+  // child id | (own type + 1) << 20 of this wave's rows (children < 2^20, types < 1023)
+  const int ct = child | ((myt + 1) << 20);
+  auto row_child = [&](int rloc, int &chd, int &mt) {  // rloc: row within the wave's 64
+    const int x = __shfl(ct, rloc & 63, WAVE);
     chd = x & 0xFFFFF;
     mt = (x >> 20) - 1;
   };
-  int obase = 0;  // overflow entries used so far
+  const int r0w = WAVE * wv;  // the wave's first row
+  const int rend = min(n, r0w + WAVE);
   const int Lh = lane >> 5, x31 = lane & 31;
   uint2 qn[MAXQ];
   int chdn, mtn;
@@ -2479,15 +2470,15 @@ __global__ __launch_bounds__(WAVE) void santa_tile_kernel(SantaArgs a, unsigned 
 #pragma unroll
   for (int t = 0; t < MAXQ; ++t) qn[t] = load_chunk(a.wish + (size_t)chdn * nw, cb + t);
 #pragma unroll 1
-  for (int s0 = 0; s0 < n && fits; s0 += RPS) {
+  for (int s0 = r0w; s0 < rend; s0 += RPS) {
     const int row = s0 + qr;
     const bool lr = row < n;
     const int mt = mtn;
     uint2 q[MAXQ];
 #pragma unroll
     for (int t = 0; t < MAXQ; ++t) q[t] = qn[t];
-    if (s0 + RPS < n) {
-      row_child(s0 + RPS + qr, chdn, mtn);
+    if (s0 + RPS < rend) {
+      row_child(s0 + RPS - r0w + qr, chdn, mtn);
 #pragma unroll
       for (int t = 0; t < MAXQ; ++t) qn[t] = load_chunk(a.wish + (size_t)chdn * nw, cb + t);
     }
@@ -2571,26 +2562,29 @@ __global__ __launch_bounds__(WAVE) void santa_tile_kernel(SantaArgs a, unsigned 
       const int cr = (int)off_l[rl + 1] - o0;
       if (cr > 32) {
         const int extra = cr - 31;
+        int obase = 0;
+        if (lane == 0) obase = atomicAdd(ocnt, extra);
+        obase = __builtin_amdgcn_readfirstlane(obase);
         if (obase + extra > a.cap) {  // a.cap <= SP2_OVF_CAP (tests lower it)
           fits = false;
           break;
         }
         for (int x = lane; x < extra; x += WAVE) rovf[obase + x] = (uint16_t)tile_entry(hits[o0 + 31 + x]);
         if (lane == 0) rovfr[s0 + rl] = (uint32_t)obase | ((uint32_t)extra << 16);
-        obase += extra;
       }
     }
+    if (!fits) break;
   }
-  if (!fits) {  // does not fit: leave the block to the fallback kernel
-    if (lane == 0) {
+  if (__syncthreads_or(!fits)) {  // does not fit: leave the block to the fallback kernel
+    if (tid == 0) {
       *status = 1;
       const int p = atomicAdd(a.ovf_cnt, 1);
       a.ovf_list[p] = b;
     }
     return;
   }
-  ((uint32_t *)(rec + SP2_REC_OWN))[lane] = ((uint32_t *)own)[lane];
-  if (lane == 0) *status = 0;
+  if (tid < 64) ((uint32_t *)(rec + SP2_REC_OWN))[tid] = ((uint32_t *)own)[tid];
+  if (tid == 0) *status = 0;
 }
 
 struct Sp2Lds {
@@ -3688,9 +3682,9 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
     // (budget / 16 entries) so that some or all blocks take the fallback
     a.cap = ctx->sp_budget > 0 ? std::min(SP2_OVF_CAP, ctx->sp_budget / 16) : SP2_OVF_CAP;
     if (vec)
-      hipLaunchKernelGGL(santa_tile_kernel<true>, dim3(B), dim3(WAVE), lds, s, a, ctx->d_rec);
+      hipLaunchKernelGGL(santa_tile_kernel<true>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
     else
-      hipLaunchKernelGGL(santa_tile_kernel<false>, dim3(B), dim3(WAVE), lds, s, a, ctx->d_rec);
+      hipLaunchKernelGGL(santa_tile_kernel<false>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(santa_sp2_kernel, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
                        (const unsigned char *)ctx->d_rec);
