@@ -41,7 +41,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", choices=["single", "twins"], default="single")
+    ap.add_argument("--mode", choices=["single", "twins", "triplets"], default="single",
+                    help="triplets: the 3-slot unit extension (not a reference script)")
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--seed", type=int, default=2017)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -122,11 +123,14 @@ def cpu_baseline(sd, mode: int, n: int, seconds: float, cores: int):
     import concurrent.futures as cf
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    from santa_hip.sampler import sample_blocks, single_geometry, twin_geometry
+    from santa_hip.sampler import sample_blocks, single_geometry, triplet_geometry, twin_geometry
     tri, tw = sd.families
     if mode == 0:
         lo, count, nb = single_geometry(sd.nc, n, tri, tw)
         stride = 1
+    elif mode == 2:
+        lo, count, nb = triplet_geometry(tri, n)
+        stride = 3
     else:
         lo, count, nb = twin_geometry(tri, tw, n)
         stride = 2
@@ -198,11 +202,12 @@ def scipy_baseline(sd, mode, n, seconds, ncores, rows, lo, count, stride, nb):
         if time.perf_counter() > deadline:
             return 0
         t = types[block]
-        T = table(block) if mode == 0 else table(block) + table(block + 1)
+        T = table(block)
+        for m in range(1, mode + 1):  # float32, left to right (mpi_twins.py:101)
+            T = T + table(block + m)
         _, col = linear_sum_assignment(T[:, t].astype(np.float64))
-        types[block] = t[col]
-        if mode == 1:
-            types[block + 1] = t[col]
+        for m in range(mode + 1):
+            types[block + m] = t[col]
         return 1
 
     deadline = time.perf_counter() + seconds
@@ -272,7 +277,9 @@ def main():
     cpu = cpu_info()
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     # B1 first, in a child process, while nothing here has touched the GPU
-    b1 = b1_baseline(args.mode, args.n, cpu["used"], args.b1_seconds) if want_cpu else None
+    # (the reference has no triplet script: no B1 for the triplet extension)
+    b1 = (b1_baseline(args.mode, args.n, cpu["used"], args.b1_seconds)
+          if want_cpu and args.mode != "triplets" else None)
 
     import torch
     import santa_hip
@@ -290,7 +297,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
         else:
             dist.init_process_group(args.dist_backend)
-    mode = _lib.SH_MODE_SINGLE if args.mode == "single" else _lib.SH_MODE_TWINS
+    mode = {"single": _lib.SH_MODE_SINGLE, "twins": _lib.SH_MODE_TWINS,
+            "triplets": _lib.SH_MODE_TRIPLETS}[args.mode]
     n = args.n
     sd = D.synthetic(args.seed)
     ctx = SantaGPU.from_data(sd, local)
@@ -331,7 +339,7 @@ def main():
 
     def step(rnd: int, timed: bool):
         rows = ctx.sample_blocks(mode, n, nb, args.seed, rnd)
-        if mode == _lib.SH_MODE_TWINS:
+        if mode != _lib.SH_MODE_SINGLE:
             backup.copy_(types)
         if timed:
             e0 = torch.cuda.Event(enable_timing=True)
@@ -418,7 +426,7 @@ def main():
     # -- roofline of the dominant kernel (fused cost build + SAP + apply) ------
     design = ctx.solve_design(mode, n, max(my_blocks, 1))
     kname = _lib.SH_DESIGN_NAMES[design]
-    per_block = (208 if mode == 0 else 408) * n  # algorithmic HBM bytes / block
+    per_block = (200 * (mode + 1) + 8) * n  # algorithmic HBM bytes / block
     achieved = per_block * my_blocks / kern_avg_s / 1e9 if kern_avg_s > 0 else 0.0
     # latency / occupancy view from the Dijkstra steps of the TIMED launches:
     # the kernel is a serial chain of Dijkstra steps per block.  The lone
@@ -478,6 +486,8 @@ def main():
                                 + (" (BASELINE config 2)" if n == 256 else " (reference block size)"
                                    if n == 2000 else "")
                                 if mode == 0 else
+                                f"triplets full round: {nb} disjoint {n}-unit blocks/round (extension)"
+                                if mode == 2 else
                                 f"twins full round: {nb} disjoint {n}-pair blocks/round"
                                 + (" (BASELINE config 3)" if n == 256 else " (reference block size)"
                                    if n == 3000 else "")),

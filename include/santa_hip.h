@@ -39,6 +39,10 @@ extern "C" {
 
 #define SH_MODE_SINGLE 0 /* rows are child ids            (mpi_single.py)  */
 #define SH_MODE_TWINS 1  /* rows are first-twin ids c, c+1 (mpi_twins.py)  */
+#define SH_MODE_TRIPLETS 2 /* rows are first-triplet ids c, c+1, c+2: 3-slot
+                              units, cost float32((h1 + h2) + h3) (extension:
+                              the reference only asserts triplets,
+                              mpi_single.py:32-37)                          */
 
 #define SH_COMPAT_TIEBREAK 1u /* scipy's exact tie-break (always on) */
 /* Test/profiling flags (same results, different code path or phases):     */
@@ -186,7 +190,8 @@ int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream);
  * Multi-GPU exchange helpers (the reference's comm.send/recv + comm.bcast of
  * results, mpi_single.py:136-147, becomes one RCCL all-gather of these):
  *   sh_pack_types:   d_out[k]        = d_types[d_rows[k]]        k < count
- *   sh_unpack_types: d_types[d_rows[k]] = d_in[k]  (twins: also d_rows[k]+1)
+ *   sh_unpack_types: d_types[d_rows[k] + m] = d_in[k] for m <= mode (twins:
+ *                    also d_rows[k]+1; triplets: +1 and +2)
  * rows < 0 are skipped (padding).
  * ------------------------------------------------------------------------ */
 int sh_pack_types(const int16_t *d_types, const int32_t *d_rows, int count,

@@ -251,6 +251,24 @@ __device__ __forceinline__ int64_t twin_cost(uint32_t code16, int nw1, int64_t E
   return (int64_t)(-a) * 4294967296LL + m;
 }
 
+// Triplets (3-slot units, extension of mpi_twins.py:99-102 to the reference's
+// triplet families, mpi_single.py:32-37): C = (h1 + h2) + h3 evaluated in
+// float32 as numpy does, left to right, one rounding per add (RNE; the
+// library is built with -ffp-contract=off).  Every float32 value here is a
+// multiple of 2^-31 (|h| >= the miss value 2^-8 * 1.28), so units are exact.
+// code24 = c1 | c2 << 8 | c3 << 16.
+__device__ __forceinline__ int64_t triplet_cost(uint32_t code24, int nw1, int64_t E) {
+  const float miss = (float)E * 4.656612873077393e-10f;  // E * 2^-31 (exact: E < 2^24)
+  float h[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int c = (int)((code24 >> (8 * m)) & 0xFFu);
+    h[m] = c ? (float)(-2 * (nw1 - c)) : miss;
+  }
+  const float s = __fadd_rn(__fadd_rn(h[0], h[1]), h[2]);
+  return (int64_t)((double)s * 2147483648.0);
+}
+
 __device__ __forceinline__ int64_t single_cost(uint32_t code, int nw1, int64_t E) {
   return code ? (int64_t)((int)code - nw1) * 4294967296LL : E;
 }
@@ -2919,14 +2937,16 @@ struct WishRowLoader {
   const int32_t *rows;    // LDS [n]
   const uint32_t *thead;  // LDS [ng]: end in csort | count << 16
   const uint16_t *csort;  // LDS [n]
-  uint8_t *rowbuf;        // LDS [n] (singles) / [2n] (twins: c1 | c2 << 8)
+  uint8_t *rowbuf;        // LDS [n] (singles) / [2n] (twins: c1 | c2 << 8) / [4n] (triplets)
   int n, nw, nw1;
   int64_t E;
+  static constexpr int M = MODE + 1;                     // children per unit
+  static constexpr int BPC = MODE == 0 ? 1 : 2 * MODE;  // rowbuf bytes per column
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int nch = (nw + 3) >> 2;
-    if (tid < (MODE ? 2 : 1) * nch) {
-      const int vr = MODE ? (tid >= nch) : 0;
+    if (tid < M * nch) {
+      const int vr = tid / nch;  // member of the unit
       const int cc = tid - vr * nch;
       const int16_t *src = wish + (size_t)(rows[i] + vr) * nw;
       uint32_t g4[4];
@@ -2944,7 +2964,7 @@ struct WishRowLoader {
           const uint32_t h = thead[g];
           const int cnt = (int)(h >> 16), e = (int)(h & 0xFFFFu);
           const uint8_t code = (uint8_t)(4 * cc + z + 1);
-          for (int x = e - cnt; x < e; ++x) rowbuf[MODE ? 2 * csort[x] + vr : csort[x]] = code;
+          for (int x = e - cnt; x < e; ++x) rowbuf[BPC * csort[x] + vr] = code;
         }
       }
     }
@@ -2953,7 +2973,11 @@ struct WishRowLoader {
     for (int k = 0; k < K; ++k) {
       const int j = w * (WAVE * K) + k * WAVE + lane;
       if (j < n) {
-        if (MODE) {
+        if (MODE == 2) {
+          uint32_t *rb = (uint32_t *)rowbuf;
+          c[k] = triplet_cost(rb[j], nw1, E);
+          rb[j] = 0;
+        } else if (MODE == 1) {
           uint16_t *rb = (uint16_t *)rowbuf;
           c[k] = twin_cost(rb[j], nw1, E);
           rb[j] = 0;
@@ -2984,7 +3008,7 @@ __host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int n
   L.ctype = o;  o += r16((size_t)n * 2);
   L.csort = o;  o += r16((size_t)n * 2);
   L.thead = o;  o += r16((size_t)ng * 4);
-  L.rowbuf = o; o += r16((size_t)n * (mode ? 2 : 1));
+  L.rowbuf = o; o += r16((size_t)n * (mode == 0 ? 1 : 2 * mode));
   L.part = o;   o += r16((size_t)nw * 3 * 8);
   L.scan = o;   o += r16((size_t)nw * 4);
   L.total = o;
@@ -3029,7 +3053,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
     return;
   }
   for (int t = tid; t < a.ng; t += WG) thead[t] = 0u;
-  for (int q = tid; q < n * (MODE ? 2 : 1); q += WG) rowbuf[q] = 0;
+  for (int q = tid; q < n * WishRowLoader<MODE, NW, K>::BPC; q += WG) rowbuf[q] = 0;
   for (int i = tid; i < n; i += WG) {
     S.u[i] = 0;
     S.c4r[i] = -1;
@@ -3093,6 +3117,14 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
       cost += single_cost(n1, nw1, a.E);
       dch += child_happy(n1, nw1) - child_happy(o1, nw1);
       if (a.delta) dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
+    } else if (MODE == 2) {
+      const uint32_t n2 = wish_code(a, child + 1, tnew), o2 = wish_code(a, child + 1, told);
+      const uint32_t n3 = wish_code(a, child + 2, tnew), o3 = wish_code(a, child + 2, told);
+      cost += triplet_cost(n1 | (n2 << 8) | (n3 << 16), nw1, a.E);
+      dch += child_happy(n1, nw1) + child_happy(n2, nw1) + child_happy(n3, nw1) -
+             child_happy(o1, nw1) - child_happy(o2, nw1) - child_happy(o3, nw1);
+      if (a.delta)
+        for (int m = 0; m < 3; ++m) dgh += gift_happy(a, child + m, tnew) - gift_happy(a, child + m, told);
     } else {
       const uint32_t n2 = wish_code(a, child + 1, tnew), o2 = wish_code(a, child + 1, told);
       cost += twin_cost(n1 | (n2 << 8), nw1, a.E);
@@ -3113,8 +3145,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
   __syncthreads();  // every old type was read from ctype (LDS): apply in place
   for (int i = tid; i < n; i += WG) {
     const int16_t tnew = ctype[S.c4r[i]];
-    a.types[rows_l[i]] = tnew;
-    if (MODE) a.types[rows_l[i] + 1] = tnew;
+    for (int m = 0; m <= MODE; ++m) a.types[rows_l[i] + m] = tnew;
   }
   if (tid == 0) {
     int64_t tc = 0, t0 = 0, t1 = 0;
@@ -3347,8 +3378,7 @@ __global__ void unpack_kernel(int16_t *types, const int32_t *rows, int count, co
   if (k < count) {
     const int r = rows[k];
     if (r >= 0) {
-      types[r] = in[k];
-      if (mode) types[r + 1] = in[k];
+      for (int m = 0; m <= mode; ++m) types[r + m] = in[k];
     }
   }
 }
@@ -3729,7 +3759,8 @@ int lds_tile_slots(sh_ctx *ctx, int n) {
 }
 
 int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
-  if (n > 256) return SH_DESIGN_LARGE;
+  // triplets (a few blocks per round: 1667 units) rebuild each row from the wishlists
+  if (n > 256 || mode == SH_MODE_TRIPLETS) return SH_DESIGN_LARGE;
   // twins keep the LDS tile: their 128-dword register column does not stay
   // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
   if (mode == SH_MODE_TWINS) return SH_DESIGN_TWINS;
@@ -3775,7 +3806,9 @@ int big_resident(const sh_ctx *ctx, int n) {  // mirrors launch_santa_big's conf
 
 int resident_blocks(sh_ctx *ctx, int design, int mode, int n) {
   switch (design) {
-    case SH_DESIGN_LARGE: return mode == SH_MODE_SINGLE ? big_resident<0>(ctx, n) : big_resident<1>(ctx, n);
+    case SH_DESIGN_LARGE:
+      return mode == SH_MODE_SINGLE ? big_resident<0>(ctx, n)
+             : mode == SH_MODE_TWINS ? big_resident<1>(ctx, n) : big_resident<2>(ctx, n);
     case SH_DESIGN_TWINS:
       return occ_blocks(ctx, santa_block_kernel<1, 1>, SANTA_WG, santa_lds_layout(n, 1, ctx->ng).total);
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
@@ -3794,9 +3827,10 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
                     int32_t *d_col, int64_t *d_cost, int64_t *d_delta, int64_t *d_steps,
                     unsigned flags, void *stream) {
   if (!ctx || (!d_rows && B > 0) || !d_types) return fail(SH_ERR_ARGS, "null pointer");
-  if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS) return fail(SH_ERR_ARGS, "bad mode");
+  if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS && mode != SH_MODE_TRIPLETS)
+    return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA) return fail(SH_ERR_ARGS, "n must be in [1, 4096]");
-  if ((int64_t)n * (mode ? 2 : 1) > ctx->nc) return fail(SH_ERR_ARGS, "block larger than the instance");
+  if ((int64_t)n * (mode + 1) > ctx->nc) return fail(SH_ERR_ARGS, "block larger than the instance");
   if (B < 0) return fail(SH_ERR_ARGS, "B < 0");
   if (B == 0) return SH_OK;
   DeviceGuard dg(ctx->device);
@@ -3810,7 +3844,9 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   hipStream_t s = (hipStream_t)stream;
   switch (pick_design(ctx, mode, n, B, flags)) {
     case SH_DESIGN_LARGE:
-      return mode == SH_MODE_SINGLE ? launch_santa_big<0>(ctx, a, B, s) : launch_santa_big<1>(ctx, a, B, s);
+      return mode == SH_MODE_SINGLE ? launch_santa_big<0>(ctx, a, B, s)
+             : mode == SH_MODE_TWINS ? launch_santa_big<1>(ctx, a, B, s)
+                                     : launch_santa_big<2>(ctx, a, B, s);
     case SH_DESIGN_TWINS: return launch_santa<1, 1>(ctx, a, B, s);
     case SH_DESIGN_LDS_TILE: return launch_santa<1, 0>(ctx, a, B, s);
     case SH_DESIGN_SW_TILE: return launch_santa_sw(ctx, a, B, s);
@@ -3822,7 +3858,8 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
 
 int sh_solve_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   if (!ctx) return fail(SH_ERR_ARGS, "null ctx");
-  if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS) return fail(SH_ERR_ARGS, "bad mode");
+  if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS && mode != SH_MODE_TRIPLETS)
+    return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA || B < 0) return fail(SH_ERR_ARGS, "bad n or B");
   DeviceGuard dg(ctx->device);
   return pick_design(ctx, mode, n, B, flags);
@@ -3830,7 +3867,8 @@ int sh_solve_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
 
 int sh_resident_blocks(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   if (!ctx) return fail(SH_ERR_ARGS, "null ctx");
-  if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS) return fail(SH_ERR_ARGS, "bad mode");
+  if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS && mode != SH_MODE_TRIPLETS)
+    return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA || B < 0) return fail(SH_ERR_ARGS, "bad n or B");
   DeviceGuard dg(ctx->device);
   return resident_blocks(ctx, pick_design(ctx, mode, n, B, flags), mode, n);
@@ -3877,6 +3915,7 @@ int sh_pack_types(const int16_t *d_types, const int32_t *d_rows, int count, int1
 int sh_unpack_types(int16_t *d_types, const int32_t *d_rows, int count, const int16_t *d_in,
                     int mode, void *stream) {
   if (count < 0) return fail(SH_ERR_ARGS, "count < 0");
+  if (mode < SH_MODE_SINGLE || mode > SH_MODE_TRIPLETS) return fail(SH_ERR_ARGS, "bad mode");
   if (count == 0) return SH_OK;
   hipLaunchKernelGGL(unpack_kernel, dim3((count + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      d_types, d_rows, count, d_in, mode);

@@ -18,6 +18,7 @@ SH_ERR_ARGS = -2
 SH_ERR_HIP = -3
 SH_MODE_SINGLE = 0
 SH_MODE_TWINS = 1
+SH_MODE_TRIPLETS = 2  # extension: 3-slot triplet units (the reference only asserts them)
 SH_COMPAT_TIEBREAK = 1
 SH_FLAG_EXACT_ARGMIN = 2
 SH_FLAG_BUILD_ONLY = 4

@@ -5,6 +5,7 @@ module globals:
   avg_normalized_happiness(pred, child_pref, gift_pref)   mpi_single.py:13-83
   optimize_block(child_block, current_gift_ids)           mpi_single.py:93-102
   optimize_block_twins(child_block, subm)                 mpi_twins.py:93-105
+and the triplet extension optimize_block_triplets(child_block, subm).
 `init(child_data, gift_data)` plays the role of the module set-up
 (mpi_single.py:193-220): it uploads the tables once into a SantaGPU context
 that the three functions then use, exactly as the reference's functions read
@@ -112,4 +113,19 @@ def optimize_block_twins(child_block, subm):
     gifts = subm["GiftId"].to_numpy() if hasattr(subm, "columns") else np.asarray(subm)
     gift_block = gifts[child_block]
     col = _solve_one(_lib.SH_MODE_TWINS, child_block, gifts.astype(np.int64))
+    return child_block, gift_block[col]
+
+
+def optimize_block_triplets(child_block, subm):
+    """Triplet extension of optimize_block_twins (mpi_twins.py:93-105 with
+    three members): rows are first triplets c (units c, c+1, c+2), columns
+    take the first triplet's GiftId, C[i, j] = float32((h(c) + h(c+1)) +
+    h(c+2)).  The reference never optimises triplets (it only asserts that
+    they share a gift, mpi_single.py:32-37).
+    -> (child_block[row_ind], gift_block[col_ind])."""
+    s = session()
+    child_block = np.asarray(child_block).astype(np.int64)
+    gifts = subm["GiftId"].to_numpy() if hasattr(subm, "columns") else np.asarray(subm)
+    gift_block = gifts[child_block]
+    col = _solve_one(_lib.SH_MODE_TRIPLETS, child_block, gifts.astype(np.int64))
     return child_block, gift_block[col]

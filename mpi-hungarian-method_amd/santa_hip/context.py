@@ -16,7 +16,7 @@ import torch
 
 from . import _lib
 from .data import SantaData
-from .sampler import family_sizes, single_geometry, twin_geometry
+from .sampler import family_sizes, single_geometry, triplet_geometry, twin_geometry
 
 
 def _ptr(t: torch.Tensor | None):
@@ -95,6 +95,9 @@ class SantaGPU:
         if mode == _lib.SH_MODE_SINGLE:
             lo, count, nb = single_geometry(self.nc, n, self.n_triplets, self.n_twins)
             return lo, count, 1, nb
+        if mode == _lib.SH_MODE_TRIPLETS:
+            lo, count, nb = triplet_geometry(self.n_triplets, n)
+            return lo, count, 3, nb
         lo, count, nb = twin_geometry(self.n_triplets, self.n_twins, n)
         return lo, count, 2, nb
 

@@ -83,6 +83,15 @@ def twin_geometry(n_triplets: int, n_twins: int, pairs: int):
     return n_triplets, n_blocks * pairs, n_blocks
 
 
+def triplet_geometry(n_triplets: int, units: int):
+    """(lo, count, n_blocks) for triplet blocks (an extension: the reference
+    never moves triplets, it asserts they share a gift, mpi_single.py:32-37).
+    Units are first-triplet ids 0, 3, ..., n_triplets - 3 (mpi_single.py:27-28
+    puts the triplets first); a block holds `units` of them."""
+    count = n_triplets // 3
+    return 0, count, count // units
+
+
 def sample_blocks(seed: int, round_: int, lo: int, count: int, stride: int, n: int, B: int) -> np.ndarray:
     """Host mirror of sh_sample_blocks -> int32 [B, n] row ids."""
     if B * n > count:

@@ -182,6 +182,31 @@ void oracle_cost_twins(const int16_t *wish, int n_wish, int ng, const int16_t *t
     free(t1); free(t2);
 }
 
+/* Triplet extension (the reference only asserts triplets, mpi_single.py:
+ * 32-37): rows[i] = first triplet c1 (units c1, c1+1, c1+2), column gift =
+ * types[rows[j]], C = float32(float32(h(c1,g) + h(c1+1,g)) + h(c1+2,g)):
+ * optimize_block_twins' expression (mpi_twins.py:101) with a third member,
+ * evaluated left to right in float32 as numpy does for float32 scalars.     */
+void oracle_cost_triplets(const int16_t *wish, int n_wish, int ng, const int16_t *types,
+                          const int32_t *rows, int n, int64_t *C)
+{
+    float *t1 = (float *)malloc((size_t)ng * sizeof(float));
+    float *t2 = (float *)malloc((size_t)ng * sizeof(float));
+    float *t3 = (float *)malloc((size_t)ng * sizeof(float));
+    for (int i = 0; i < n; ++i) {
+        happy_row(wish + (int64_t)rows[i] * n_wish, n_wish, ng, t1);
+        happy_row(wish + ((int64_t)rows[i] + 1) * n_wish, n_wish, ng, t2);
+        happy_row(wish + ((int64_t)rows[i] + 2) * n_wish, n_wish, ng, t3);
+        for (int j = 0; j < n; ++j) {
+            int g = types[rows[j]];
+            volatile float s12 = t1[g] + t2[g];  /* one float32 rounding per add */
+            float s = s12 + t3[g];
+            C[(int64_t)i * n + j] = to_units((double)s);
+        }
+    }
+    free(t1); free(t2); free(t3);
+}
+
 /* ------------------------------------------------------------------------ */
 /* (3) avg_normalized_happiness integer sums (mpi_single.py:13-83).          */
 /* out[0] = S_child  = sum_c (first rank r of type in wishlist ? 2*(n_wish-r) : -1)
@@ -216,7 +241,8 @@ void oracle_score(const int16_t *wish, int n_wish, const int32_t *good, int n_go
 /* ------------------------------------------------------------------------ */
 /* (4) One block-Hungarian round on the CPU: cost build + LSAP + apply.      */
 /*     mode 0 = singles (mpi_single.py:133,151-152), 1 = twins              */
-/*     (mpi_twins.py:136,154-156).  rows: B x n.  types updated in place.    */
+/*     (mpi_twins.py:136,154-156), 2 = triplets (extension: all three       */
+/*     members take the unit's new gift).  rows: B x n.  types in place.     */
 /*     col_out (B x n, nullable), cost_out (B, nullable).                    */
 /* ------------------------------------------------------------------------ */
 int oracle_round(int mode, const int16_t *wish, int n_wish, int ng, int16_t *types,
@@ -230,7 +256,8 @@ int oracle_round(int mode, const int16_t *wish, int n_wish, int ng, int16_t *typ
     for (int b = 0; b < B; ++b) {
         const int32_t *rb = rows + (int64_t)b * n;
         if (mode == 0) oracle_cost_single(wish, n_wish, ng, types, rb, n, C);
-        else oracle_cost_twins(wish, n_wish, ng, types, rb, n, C);
+        else if (mode == 1) oracle_cost_twins(wish, n_wish, ng, types, rb, n, C);
+        else oracle_cost_triplets(wish, n_wish, ng, types, rb, n, C);
         int r = oracle_lsap_i64(n, n, C, col, stats);
         if (r) { rc = r; break; }
         int64_t s = 0;
@@ -239,8 +266,7 @@ int oracle_round(int mode, const int16_t *wish, int n_wish, int ng, int16_t *typ
             newt[i] = types[rb[col[i]]];
         }
         for (int i = 0; i < n; ++i) {
-            types[rb[i]] = newt[i];
-            if (mode == 1) types[rb[i] + 1] = newt[i];
+            for (int m = 0; m <= mode; ++m) types[rb[i] + m] = newt[i];
         }
         if (col_out) for (int i = 0; i < n; ++i) col_out[(int64_t)b * n + i] = col[i];
         if (cost_out) cost_out[b] = s;

@@ -49,6 +49,7 @@ def lib():
         L.oracle_lsap_i64_batched.argtypes = [_I, _I, _P, _P, _P, _P]
         L.oracle_cost_single.argtypes = [_P, _I, _I, _P, _P, _I, _P]
         L.oracle_cost_twins.argtypes = [_P, _I, _I, _P, _P, _I, _P]
+        L.oracle_cost_triplets.argtypes = [_P, _I, _I, _P, _P, _I, _P]
         L.oracle_score.argtypes = [_P, _I, _P, _I, _I, _P, _I, _I, _P]
         L.oracle_round.argtypes = [_I, _P, _I, _I, _P, _P, _I, _I, _P, _P, _P]
         for f in (L.oracle_lsap_f64, L.oracle_lsap_i64, L.oracle_lsap_i64_batched,
@@ -135,6 +136,18 @@ def cost_twins(wish: np.ndarray, types: np.ndarray, rows: np.ndarray, ng: int | 
     C = np.zeros((n, n), dtype=np.int64)
     lib().oracle_cost_twins(_ptr(wish), wish.shape[1], _ng_of(wish, types, ng), _ptr(types),
                             _ptr(rows), n, _ptr(C))
+    return C
+
+
+def cost_triplets(wish: np.ndarray, types: np.ndarray, rows: np.ndarray, ng: int | None = None) -> np.ndarray:
+    """Triplet units (extension of mpi_twins.py:93-103 to three members)."""
+    wish = np.ascontiguousarray(wish, dtype=np.int16)
+    types = np.ascontiguousarray(types, dtype=np.int16)
+    rows = np.ascontiguousarray(rows, dtype=np.int32)
+    n = rows.shape[0]
+    C = np.zeros((n, n), dtype=np.int64)
+    lib().oracle_cost_triplets(_ptr(wish), wish.shape[1], _ng_of(wish, types, ng), _ptr(types),
+                               _ptr(rows), n, _ptr(C))
     return C
 
 

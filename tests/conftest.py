@@ -42,6 +42,11 @@ def santa_blocks():
 
 
 @pytest.fixture(scope="session")
+def santa_triplets():
+    return load_npz_cases("santa_triplets.npz")
+
+
+@pytest.fixture(scope="session")
 def full_data():
     """The seeded full-size synthetic instance the Santa fixtures were made on."""
     from santa_hip import data as D

@@ -12,7 +12,7 @@ import torch
 import oracle
 from santa_hip import _lib
 from santa_hip.context import score_from_sums
-from santa_hip.sampler import family_sizes, sample_blocks, single_geometry, twin_geometry
+from santa_hip.sampler import family_sizes, sample_blocks, single_geometry, triplet_geometry, twin_geometry
 
 
 def sha(a: np.ndarray) -> str:
@@ -33,6 +33,9 @@ class CPUOracleEngine:
         if mode == _lib.SH_MODE_SINGLE:
             lo, count, nb = single_geometry(self.nc, n, self.n_triplets, self.n_twins)
             return lo, count, 1, nb
+        if mode == _lib.SH_MODE_TRIPLETS:
+            lo, count, nb = triplet_geometry(self.n_triplets, n)
+            return lo, count, 3, nb
         lo, count, nb = twin_geometry(self.n_triplets, self.n_twins, n)
         return lo, count, 2, nb
 
@@ -53,15 +56,27 @@ class CPUOracleEngine:
         v = vals.numpy()
         m = r >= 0
         t = types.numpy()
-        t[r[m]] = v[m]
-        if mode:
-            t[r[m] + 1] = v[m]
+        for k in range(mode + 1):
+            t[r[m] + k] = v[m]
 
     def score_sums(self, types):
         t = types.numpy()
         s = oracle.score_sums(self.wish, self.good, t)
         self.score_log.append((s[0], s[1], sha(t)))
         return s
+
+    def score_begin(self, types):
+        """Pipelined-round protocol (GPUEngine.score_begin): score a snapshot."""
+        snap = types.clone()
+        eng = self
+
+        class _Handle:
+            def result(_):
+                return eng.score_sums(snap)
+
+            def restore(_, t):
+                t.copy_(snap)
+        return _Handle()
 
     def score_from_sums(self, sc, sg):
         return score_from_sums(sc, sg, self.nc, self.ng, self.n_wish, self.n_good)

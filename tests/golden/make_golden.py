@@ -201,6 +201,42 @@ def make_santa_blocks(sd: D.SantaData, out: str) -> None:
     print(f"santa_blocks: {k} blocks -> {out} ({os.path.getsize(out)} B)")
 
 
+def make_triplet_blocks(sd: D.SantaData, out: str) -> None:
+    """Triplet-unit blocks (an extension: the reference never moves triplets,
+    it asserts they share a gift, mpi_single.py:32-37).  C is the reference's
+    twins expression (mpi_twins.py:101) with a third member, summed left to
+    right over the reference's float32 child_happiness table
+    (mpi_single.py:213-218) exactly as numpy evaluates float32 scalars, and
+    solved by scipy's linear_sum_assignment (mpi_twins.py:103)."""
+    from scipy.optimize import linear_sum_assignment as lsa
+    nc, ng = sd.nc, sd.ng
+    tri, _ = sd.families
+    table = LazyHappiness(sd.wish, ng)
+    arrays = {}
+    meta = []
+    k = 0
+    for units, nb in ((256, 3), (100, 2), (37, 2), (5, 2)):
+        lo, count, _ = S.triplet_geometry(tri, units)
+        rows = S.sample_blocks(17, units, lo, count, 3, units, nb)
+        for b in range(nb):
+            blk = rows[b].astype(np.int64)
+            gift_block = sd.types[blk].astype(np.int64)
+            C = np.array([[table[c][g] + table[c + 1][g] + table[c + 2][g] for g in gift_block]
+                          for c in blk], dtype=np.float64)
+            _, col = lsa(C)
+            cost_units = int(round(C[np.arange(units), col].sum() * 2 ** 31))
+            arrays[f"wish{k}"] = np.stack([sd.wish[blk + m] for m in range(3)], axis=1)  # [units, 3, n_wish]
+            arrays[f"ctype{k}"] = sd.types[blk]
+            arrays[f"rows{k}"] = blk.astype(np.int32)
+            arrays[f"col{k}"] = col.astype(np.int16)
+            arrays[f"cunits{k}"] = np.round(C * 2 ** 31).astype(np.int64)[:, :8]  # spot entries
+            meta.append({"i": k, "mode": "triplets", "n": units, "cost_units": cost_units})
+            k += 1
+    arrays["meta"] = np.frombuffer(json.dumps(meta).encode(), dtype=np.uint8)
+    np.savez_compressed(out, **arrays)
+    print(f"triplet blocks: {k} blocks -> {out} ({os.path.getsize(out)} B)")
+
+
 def make_santa_blocks_large(sd: D.SantaData, out: str) -> None:
     """One block at each of the reference's own default sizes: 2000 singles
     (mpi_single.py:238) and 3000 twin pairs (mpi_twins.py:244, block_size
@@ -435,12 +471,14 @@ def main():
     todo = args.only.split(",")
     if "all" in todo or "lsap" in todo:
         make_lsap_cases(os.path.join(HERE, "lsap_cases.npz"))
-    if set(todo) & {"all", "blocks", "large", "score", "traj"}:
+    if set(todo) & {"all", "blocks", "large", "score", "traj", "triplets"}:
         t = time.time()
         sd = D.synthetic(2017)
         print(f"synthetic data {time.time() - t:.1f}s")
         if "all" in todo or "blocks" in todo:
             make_santa_blocks(sd, os.path.join(HERE, "santa_blocks.npz"))
+        if "all" in todo or "triplets" in todo:
+            make_triplet_blocks(sd, os.path.join(HERE, "santa_triplets.npz"))
         if "all" in todo or "large" in todo:
             make_santa_blocks_large(sd, os.path.join(HERE, "santa_blocks_large.npz"))
         if "all" in todo or "score" in todo:

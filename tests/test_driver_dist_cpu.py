@@ -4,7 +4,8 @@ The product exchange (santa_hip.driver.exchange: shard -> pack -> one
 all-gather -> unpack) and round loop run with the oracle-backed CPU engine;
 the final assignment and every per-round score must equal the single-rank
 run bit for bit (blocks are disjoint, integer sums are order-free), including
-block counts that do not divide evenly across ranks and the twins rollback."""
+block counts that do not divide evenly across ranks, the twins rollback and
+the triplet extension (mode 2)."""
 import os
 import socket
 
@@ -55,7 +56,8 @@ def _worker(rank, size, port, mode, n, bpr, rounds, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("size,mode,n,bpr", [(2, 0, 64, None), (3, 0, 100, 7), (2, 1, 16, None)])
+@pytest.mark.parametrize("size,mode,n,bpr", [(2, 0, 64, None), (3, 0, 100, 7), (2, 1, 16, None),
+                                              (2, 2, 16, None)])
 def test_multirank_equals_single_rank(size, mode, n, bpr):
     sd = D.synthetic(**SMALL)
     rounds = 3
@@ -133,3 +135,46 @@ def test_accept_modes_and_disjoint_check():
         assert_disjoint(torch.cat([rows, rows[:1]]), _lib.SH_MODE_TWINS)
     with pytest.raises(AssertionError):  # pairs (c, c+1) and (c+1, c+2) overlap
         assert_disjoint(torch.tensor([11, 12], dtype=torch.int32), _lib.SH_MODE_TWINS)
+
+
+@pytest.mark.parametrize("patience,rounds", [(-1, 4), (0, 6), (100, 3), (100, 0)])
+def test_pipelined_rounds_equal_serial(patience, rounds):
+    """The pipelined loop (round r's score overlapped with round r+1, a
+    speculative round rolled back when the stop rule fires) makes the same
+    decisions, history and final state as the serial loop."""
+    from cpu_engine import CPUOracleEngine
+    sd = D.synthetic(**SMALL)
+    out = []
+    for pipeline in (False, True):
+        eng = CPUOracleEngine(sd.wish, sd.goodkids, sd.nq)
+        t = torch.from_numpy(sd.types.copy())
+        res = run_rounds(eng, t, mode=_lib.SH_MODE_SINGLE, n=64, seed=5, max_rounds=rounds,
+                         patience=patience, world=World(), pipeline=pipeline)
+        hist = [(st.round, st.s_child, st.s_gift, st.score, st.accepted, st.best) for st in res.history]
+        out.append((t.numpy().copy(), hist, res.rounds, res.blocks_solved, res.best_score))
+    (t0, h0, r0, b0, s0), (t1, h1, r1, b1, s1) = out
+    assert np.array_equal(t0, t1)
+    assert h0 == h1 and r0 == r1 and b0 == b1 and s0 == s1
+    if patience == -1:
+        assert r0 == 1  # stopped after the first round; the speculative second was undone
+
+
+def test_triplet_rounds_keep_units():
+    """Triplet rounds (mode 2, keep-if-improved): units move whole, so every
+    triplet still shares a gift, and a rejected round leaves the state as it was."""
+    from cpu_engine import CPUOracleEngine
+    from santa_hip.driver import assert_disjoint
+    sd = D.synthetic(**SMALL)
+    eng = CPUOracleEngine(sd.wish, sd.goodkids, sd.nq)
+    _, _, stride, nb = eng.geometry(_lib.SH_MODE_TRIPLETS, 16)
+    assert stride == 3 and nb == eng.n_triplets // 3 // 16
+    t = torch.from_numpy(sd.types.copy())
+    res = run_rounds(eng, t, mode=_lib.SH_MODE_TRIPLETS, n=16, seed=2, max_rounds=3,
+                     world=World(), check_disjoint=True)
+    fam = t.numpy()[:eng.n_triplets].reshape(-1, 3)
+    assert (fam == fam[:, :1]).all()
+    assert res.rounds >= 1 and res.best_score >= res.history[0].score or not res.history[0].accepted
+    rows = eng.sample_blocks(_lib.SH_MODE_TRIPLETS, 16, 2, 1, 0)
+    assert_disjoint(rows, _lib.SH_MODE_TRIPLETS)
+    with pytest.raises(AssertionError):  # units (c, c+1, c+2) and (c+2, ...) overlap
+        assert_disjoint(torch.tensor([3, 5], dtype=torch.int32), _lib.SH_MODE_TRIPLETS)

@@ -84,7 +84,7 @@ def test_lsap_hash_vs_oracle(sh, n, mod):
 
 
 # --------------------------------------------------------------------------- sampler
-@pytest.mark.parametrize("mode,n,B", [(0, 256, 3730), (1, 256, 78), (0, 100, 50)])
+@pytest.mark.parametrize("mode,n,B", [(0, 256, 3730), (1, 256, 78), (0, 100, 50), (2, 256, 6)])
 def test_sampler_matches_host_mirror(sh, ctx, mode, n, B):
     from santa_hip.sampler import sample_blocks
     lo, count, stride, nb = ctx.geometry(mode, n)
@@ -111,6 +111,52 @@ def test_santa_blocks_golden(sh, ctx, full_data, santa_blocks):
     assert ctx.error_flags() == 0
 
 
+def test_triplet_blocks_golden(sh, ctx, full_data, santa_triplets):
+    """Triplet units (extension): scipy's col_ind and the exact cost of the
+    float32 ((h1 + h2) + h3) matrix (tests/golden/santa_triplets.npz)."""
+    z, meta = santa_triplets
+    for m in meta:
+        k, n = m["i"], m["n"]
+        types = ctx.upload_types(full_data.types)
+        col = torch.empty(n, dtype=torch.int32, device="cuda")
+        cost = torch.empty(1, dtype=torch.int64, device="cuda")
+        ctx.solve_blocks(2, torch.from_numpy(z[f"rows{k}"]).cuda(), n, types, col=col, cost=cost)
+        assert np.array_equal(col.cpu().numpy(), z[f"col{k}"].astype(np.int32)), m
+        assert int(cost.item()) == m["cost_units"], m
+        t = types.cpu().numpy()
+        r = z[f"rows{k}"]
+        assert (t[r] == t[r + 1]).all() and (t[r] == t[r + 2]).all()
+    sh.init(full_data.wish, full_data.goodkids)
+    import pandas as pd
+    subm = pd.DataFrame({"ChildId": np.arange(full_data.nc), "GiftId": full_data.types.astype(np.int64)})
+    m = meta[0]
+    blk = z[f"rows{m['i']}"].astype(np.int64)
+    cids, gids = sh.optimize_block_triplets(blk, subm)
+    assert np.array_equal(cids, blk)
+    assert np.array_equal(gids, full_data.types[blk][z[f"col{m['i']}"]].astype(np.int64))
+    assert ctx.error_flags() == 0
+
+
+@pytest.mark.parametrize("patience", [-1, 100])
+def test_pipelined_rounds_equal_serial_gpu(sh, ctx, full_data, patience):
+    """GPUEngine.score_begin (score on a side stream from a snapshot, next
+    round launched meanwhile, speculative round undone at the stop) gives the
+    serial loop's history and final state on full 3730-block rounds."""
+    from santa_hip.driver import GPUEngine, World, run_rounds
+    out = []
+    for pipeline in (False, True):
+        types = ctx.upload_types(full_data.types)
+        res = run_rounds(GPUEngine(ctx), types, mode=0, n=256, seed=8, max_rounds=3,
+                         patience=patience, world=World(), pipeline=pipeline)
+        torch.cuda.synchronize()
+        out.append((types.cpu().numpy(), [(st.round, st.s_child, st.s_gift, st.score, st.best)
+                                          for st in res.history], res.rounds))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1] and out[0][2] == out[1][2]
+    assert out[0][2] == (1 if patience == -1 else 3)
+    assert ctx.error_flags() == 0
+
+
 def test_santa_blocks_golden_reference_sizes(sh, ctx, full_data):
     """The reference's optimize_block at its default 2000 and
     optimize_block_twins at 3000 pairs (golden, made from the reference)."""
@@ -134,7 +180,9 @@ def test_santa_blocks_golden_reference_sizes(sh, ctx, full_data):
                                       # up to the reference's own sizes (mpi_single.py:238,
                                       # mpi_twins.py:244)
                                       (0, 257, 3), (0, 700, 2), (0, 1024, 2), (0, 2000, 2),
-                                      (1, 300, 2), (1, 1500, 1), (1, 3000, 1)])
+                                      (1, 300, 2), (1, 1500, 1), (1, 3000, 1),
+                                      # triplet units (extension; always the row-rebuild design)
+                                      (2, 256, 6), (2, 100, 5), (2, 37, 4), (2, 555, 3)])
 def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
     """Fused build+solve+apply on the GPU equals the CPU oracle: col, exact
     cost, the whole new type vector, and the happiness deltas."""
@@ -334,6 +382,16 @@ def test_pack_unpack_roundtrip(sh, ctx, full_data):
     r = rows.cpu().numpy()
     t2n = t2.cpu().numpy()
     assert np.array_equal(t2n[r], full_data.types[r]) and np.array_equal(t2n[r + 1], full_data.types[r])
+    # triplet units: all three members take the unit's value
+    rows3 = ctx.sample_blocks(2, 64, 5, 3, 3)
+    buf3 = torch.empty(rows3.numel(), dtype=torch.int16, device="cuda")
+    ctx.pack_types(types, rows3, buf3)
+    t3 = torch.zeros_like(types)
+    ctx.unpack_types(t3, rows3, buf3, 2)
+    r3 = rows3.cpu().numpy()
+    t3n = t3.cpu().numpy()
+    for m in range(3):
+        assert np.array_equal(t3n[r3 + m], full_data.types[r3])
 
 
 # --------------------------------------------------------------------------- argmin paths
@@ -454,6 +512,7 @@ def test_design_dispatch(sh, ctx):
     assert ctx.solve_design(1, 256, 78) == 4
     assert ctx.solve_design(0, 2000, 477) == 5
     assert ctx.solve_design(1, 3000, 6) == 5
+    assert ctx.solve_design(2, 256, 6) == 5
 
 
 # --------------------------------------------------------------------------- RCCL exchange
@@ -516,7 +575,8 @@ def test_empty_batches_are_noops(sh, ctx, full_data):
 
 
 @pytest.mark.parametrize("mode,n,B", [(0, 1, 5), (0, 2, 7), (0, 63, 3), (0, 65, 3),
-                                      (1, 1, 4), (1, 2, 3), (1, 65, 2)])
+                                      (1, 1, 4), (1, 2, 3), (1, 65, 2),
+                                      (2, 1, 4), (2, 2, 3), (2, 65, 2)])
 def test_santa_edge_block_sizes_vs_oracle(sh, ctx, full_data, mode, n, B):
     """Santa blocks of degenerate / wave-boundary sizes: the fused kernels
     equal the oracle (col, cost, whole type vector, deltas)."""
@@ -541,7 +601,7 @@ def test_santa_edge_block_sizes_vs_oracle(sh, ctx, full_data, mode, n, B):
 
 
 # --------------------------------------------------------------------------- config 4 on the HIP path
-@pytest.mark.parametrize("mode,rounds", [(0, 3), (1, 3)])
+@pytest.mark.parametrize("mode,rounds", [(0, 3), (1, 3), (2, 3)])
 def test_two_ranks_on_the_hip_path_equal_one_rank(sh, ctx, full_data, mode, rounds):
     """Config 4's sharding + exchange through GPUEngine: two ranks (one
     process each, both on cuda:0, gloo all-gather) run full rounds (3730

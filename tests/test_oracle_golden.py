@@ -7,7 +7,11 @@ Pins the oracle before it is trusted as the GPU path's checker:
                          (mpi_single.py:93-102, mpi_twins.py:93-105);
   * santa_score.json   — the reference's avg_normalized_happiness
                          (mpi_single.py:13-83) on the full synthetic instance;
-  * trajectory_*.json  — the reference's my_optimizer run for 3 rounds.
+  * trajectory_*.json  — the reference's my_optimizer run for 3 rounds;
+  * santa_triplets.npz — triplet-unit blocks (extension: the reference only
+                         asserts triplets), C from the reference's float32
+                         happiness table summed as mpi_twins.py:101 does for
+                         two members, solved by scipy.
 """
 import hashlib
 
@@ -101,6 +105,38 @@ def test_santa_blocks_cost_and_assignment(santa_blocks):
         # the float64 matrix the reference hands scipy is C * 2^-31 exactly
         _, col_f = oracle.lsap(C.astype(np.float64) / 2 ** 31)
         assert np.array_equal(col_f, col)
+
+
+def test_triplet_blocks_cost_and_assignment(santa_triplets):
+    """Triplet units: float32 ((h1 + h2) + h3), exact units, scipy's col_ind."""
+    z, meta = santa_triplets
+    for m in meta:
+        k, n = m["i"], m["n"]
+        w3 = z[f"wish{k}"]                      # [units, 3, n_wish]
+        wish = w3.reshape(3 * n, -1)
+        types = np.repeat(z[f"ctype{k}"], 3)
+        rows = 3 * np.arange(n, dtype=np.int32)
+        C = oracle.cost_triplets(wish, types, rows, ng=1000)
+        assert np.array_equal(C[:, :8], z[f"cunits{k}"]), m
+        _, col = oracle.lsap(C)
+        assert np.array_equal(col, z[f"col{k}"].astype(np.int64)), m
+        assert int(C[np.arange(n), col].sum()) == m["cost_units"], m
+
+
+def test_triplet_round_keeps_units(full_data):
+    """The oracle's triplet round moves whole units: afterwards every triplet
+    still shares a gift and the multiset of gifts is unchanged."""
+    from santa_hip import sampler as S
+    tri, _ = S.family_sizes(full_data.nc)
+    lo, count, nb = S.triplet_geometry(tri, 128)
+    rows = S.sample_blocks(3, 0, lo, count, 3, 128, nb)
+    t = full_data.types.copy()
+    col, cost = oracle.round_blocks(2, full_data.wish, t, rows, ng=full_data.ng)
+    assert nb == 13 and col.shape == (nb, 128)
+    fam = t[:tri].reshape(-1, 3)
+    assert (fam == fam[:, :1]).all()
+    assert np.array_equal(np.sort(t), np.sort(full_data.types))
+    assert oracle.score_sums(full_data.wish, full_data.goodkids, t)[2] == 0
 
 
 def test_santa_blocks_reference_sizes(full_data):
