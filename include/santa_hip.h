@@ -64,6 +64,10 @@ extern "C" {
 #define SH_FLAG_SP1 256u        /* force the sparse kernel with LDS hit lists
                                    (santa_sp_kernel) instead of the register
                                    hit tile (A/B; identical results)       */
+#define SH_FLAG_TEST_RANGE 512u /* test hook: the register-tile sparse solver
+                                   treats every block as outside its
+                                   scaled-unit range, so all blocks take the
+                                   fallback launch (same results)          */
 
 /* Kernel designs sh_solve_blocks can dispatch to (sh_solve_design).        */
 #define SH_DESIGN_SPARSE 0   /* one wave per block, hit lists in LDS        */

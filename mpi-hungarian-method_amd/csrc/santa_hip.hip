@@ -2605,6 +2605,14 @@ __global__ __launch_bounds__(TILE_NW * WAVE) void santa_tile_kernel(SantaArgs a,
   if (tid == 0) *status = 0;
 }
 
+// santa_sp2_kernel's scaled units (see its solve loop): shift, key tie-break
+// field (class 1 | position key 8 | row-or-column 8 bits, n <= 256), bias
+// (keeps sb > 0: spc >= -n_wish * 2^32 units > -2^39), magnitude bound.
+constexpr int SP2_SH = 17;
+constexpr uint32_t SP2_TIE_MASK = (1u << SP2_SH) - 1u;
+constexpr uint64_t SP2_BIAS = 1ull << (39 + SP2_SH);
+constexpr int64_t SP2_LIM = 1ll << (42 + SP2_SH);
+
 struct Sp2Lds {
   size_t ctype, own, ovfr, ovf, u, rem, rowc, total;
 };
@@ -2673,7 +2681,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
   const int nw1 = a.n_wish + 1;
   const int64_t E = a.E;
   {
-    const u64x2 E2 = {(uint64_t)E, (uint64_t)E};
+    const u64x2 E2 = {(uint64_t)E << SP2_SH, (uint64_t)E << SP2_SH};
     *(u64x2 *)(rowc + 4 * lane) = E2;
     *(u64x2 *)(rowc + 4 * lane + 2) = E2;
   }
@@ -2681,9 +2689,18 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
   const uint64_t m1 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
 
   // -- solve (santa_sp_kernel's step; the row's hits come from the tile) -----------
+  // Scaled units: every cost, dual and path length is held times 2^SP2_SH, so
+  // the low SP2_SH bits of sb = spc + BIAS are zero and the argmin key is
+  // sb | tie-break bits -- exact, one OR per column (no clamp, no saturated
+  // band, no fallback argmin).  Exact while |values| < 2^(63 - SP2_SH - 2)
+  // units: Santa duals stay within 200 happiness units (2^38.7 units,
+  // measured), the row duals only grow and the column duals only fall, so
+  // the final duals and every Dijkstra's minVal bound all intermediate values;
+  // a block outside the range (or every block under SH_FLAG_TEST_RANGE) is
+  // left untouched and re-solved by the fallback launch.
   const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
-  const uint64_t BIAS = (uint64_t)KEY_BIAS;
-  int64_t sb[4], W[4];  // spc + BIAS; -v   (columns 4*lane + k)
+  const uint64_t BIAS = SP2_BIAS;
+  int64_t sb[4], W[4];  // spc + BIAS; -v   (columns 4*lane + k), scaled
   i32x4 path, r4c;
   uint32_t c4r = ~0u;   // column of row 4*lane + k in byte k (0xFF: none yet)
   uint32_t lo[4];
@@ -2699,6 +2716,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
   for (int k = 0; k < 4; ++k) rem0 |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
   int steps = 0;
   int fallbacks = 0;
+  bool mvbig = (a.flags & SH_FLAG_TEST_RANGE) != 0;  // a Dijkstra's minVal out of range
   if (a.flags & SH_FLAG_BUILD_ONLY) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) r4c[k] = 4 * lane + k;
@@ -2716,8 +2734,8 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         const int j = 4 * ln + k;
         const int pos = n - 1 - j;
         sb[k] = smax;
-        lo[k] = (r4c[k] < 0) ? (((uint32_t)(1023 - pos) << 10) | (uint32_t)j)
-                             : ((1u << 20) | ((uint32_t)pos << 10) | (uint32_t)r4c[k]);
+        lo[k] = (r4c[k] < 0) ? (((uint32_t)(255 - pos) << 8) | (uint32_t)j)
+                             : ((1u << 16) | ((uint32_t)pos << 8) | (uint32_t)r4c[k]);
         LM[k] = __builtin_amdgcn_ballot_w64(j < n);
       }
       ((uint32_t *)rem)[lane] = rem0;
@@ -2746,24 +2764,24 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         for (int k = 0; k < 4; ++k) lo[k] ^= (4 * lane + k == kmover) ? kX : 0u;
         // expand the row: hit columns get -a << 32, the rest hold E
         const int sslot = mine ? (int)(e & 0x1FFu) : 256 + x31;
-        rowc[sslot] = (uint64_t)(uint32_t)(-(int)ea) << 32;
+        rowc[sslot] = (uint64_t)(uint32_t)(-(int)ea) << (32 + SP2_SH);
         const bool ovr = __builtin_amdgcn_ballot_w64(mine && ea == SP2_MARK) != 0;
         if (__builtin_expect(ovr, 0)) {
           const uint32_t rg = ovfr[i];  // more than 32 hits: the rest from the overflow area
           const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
           for (int x = lane; x < oc; x += WAVE) {
             const uint32_t e2 = ovf[os + x];
-            rowc[e2 & 0x1FFu] = (uint64_t)(uint32_t)(-(int)(e2 >> 9)) << 32;
+            rowc[e2 & 0x1FFu] = (uint64_t)(uint32_t)(-(int)(e2 >> 9)) << (32 + SP2_SH);
           }
         }
         const u64x2 c01 = *(const u64x2 *)(rowc + 2 * lane);
         const u64x2 c23 = *(const u64x2 *)(rowc + 128 + 2 * lane);
         // un-scatter: the slots written above get E back (in-order LDS: after the reads)
-        rowc[sslot] = (uint64_t)E;
+        rowc[sslot] = (uint64_t)E << SP2_SH;
         if (__builtin_expect(ovr, 0)) {
           const uint32_t rg = ovfr[i];
           const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
-          for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = (uint64_t)E;
+          for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = (uint64_t)E << SP2_SH;
         }
         const uint64_t cc[4] = {c01[0], c01[1], c23[0], c23[1]};
         // u~[i] = u[i] - minVal (row i is reached at the current minimum)
@@ -2781,18 +2799,13 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
           const bool upd = (int64_t)r < sb[k];
           sb[k] = upd ? (int64_t)r : sb[k];
           path[k] = upd ? i : path[k];
-          const uint32_t sh = (uint32_t)((uint64_t)sb[k] >> 32), sl = (uint32_t)sb[k];
-          // bits 11..42 of sb (sb > 0 here: spc >= min C - v >= -n_wish * 2^32
-          // > -BIAS); from sb >= 2047 * 2^32 the key saturates at >= 0xFFE00000
-          // and a saturated winner is re-decided by the exact argmin below
-          const uint32_t kh = __builtin_amdgcn_alignbit(min(sh, 2047u), sl, 11);
-          const uint64_t key = ((uint64_t)kh << 32) | ((sl << 21) | lo[k]);
+          // (sb > 0: spc >= min C - v >= -n_wish * 2^32 units > -BIAS)
+          const uint64_t key = (uint64_t)sb[k] | lo[k];
           best = (lv && key < best) ? key : best;
         }
         uint64_t g = rfl_u64(wave_min_u64_fast(best));
-        const uint32_t ghi = (uint32_t)(g >> 32);
-        if (exact || ghi - 1u >= 0xFFDFFFFFu) {  // saturated key (0, or >= 0xFFE00000)
-          // exact two-pass argmin: min sb (signed), then min tie-break bits
+        if (exact) {
+          // two-pass argmin (test path): min sb, then min tie-break bits
           uint64_t m = ~0ull;
 #pragma unroll
           for (int k = 0; k < 4; ++k)
@@ -2803,23 +2816,21 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             if (__builtin_amdgcn_inverse_ballot_w64(LM[k]) && sb[k] == ms) b2 = umin64(b2, (uint64_t)lo[k]);
-          g = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wave_min_u64_dpp(b2));
-          minVal = (int64_t)((uint64_t)ms - BIAS);
+          g = (uint64_t)ms | (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wave_min_u64_dpp(b2));
           ++fallbacks;
-        } else {
-          minVal = (int64_t)((g >> KEY_LO_BITS) - BIAS);
         }
-        const uint32_t glo = (uint32_t)g & 0x1FFFFFu;
-        const bool assigned = (glo >> 20) & 1u;
-        const int pk = (int)((glo >> 10) & 1023u);
-        const int aux = (int)(glo & 1023u);
-        const int pstar = assigned ? pk : 1023 - pk;
+        minVal = (int64_t)((g & ~(uint64_t)SP2_TIE_MASK) - BIAS);
+        const uint32_t glo = (uint32_t)g & SP2_TIE_MASK;
+        const bool assigned = (glo >> 16) & 1u;
+        const int pk = (int)((glo >> 8) & 255u);
+        const int aux = (int)(glo & 255u);
+        const int pstar = assigned ? pk : 255 - pk;
         const int last = nrem - 1;
         // the winner leaves `remaining`; the column at `last` moves to pstar
         // (applied to the registers at the top of the next step)
         const int mover = __builtin_amdgcn_readfirstlane(mover_v);
         kglo = glo;
-        kX = (uint32_t)(last ^ pstar) << 10;
+        kX = (uint32_t)(last ^ pstar) << 8;
         kmover = mover;
         rem[pstar] = (uint8_t)mover;  // (every lane, same byte; a no-op when pstar == last)
         --nrem;
@@ -2846,6 +2857,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         if (vk && r4c[k] >= 0) u_l[r4c[k]] += d;
       }
       if (lane == 0) u_l[cur] += minVal;
+      mvbig |= (uint64_t)(minVal + SP2_LIM) >= 2 * (uint64_t)SP2_LIM;
       // augment along path[] from the sink back to cur (registers only)
       int j = sink;
       for (;;) {
@@ -2871,6 +2883,21 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
   }
   __syncthreads();
 
+  {  // the scaled-unit range (see the solve loop): leave the block to the fallback
+    bool big = mvbig;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      big |= (uint64_t)(W[k] + SP2_LIM) >= 2 * (uint64_t)SP2_LIM;
+      if (4 * lane + k < n) big |= (uint64_t)(u_l[4 * lane + k] + SP2_LIM) >= 2 * (uint64_t)SP2_LIM;
+    }
+    if (__builtin_expect(__any(big), 0)) {
+      if (lane == 0) {
+        const int p = atomicAdd(a.ovf_cnt, 1);
+        a.ovf_list[p] = b;
+      }
+      return;
+    }
+  }
   const uint64_t m2 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
   // -- outputs: lane handles rows i = 4*lane + k ------------------------------------
   int64_t cost = 0, dch = 0, dgh = 0;
@@ -2890,7 +2917,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
       if (a.flags & SH_FLAG_BUILD_ONLY) {
         cost += single_cost(co, nw1, E);
       } else {
-        const int64_t cij = u_l[i] + vcol;  // = C[i][col] (tight matched edge)
+        const int64_t cij = (u_l[i] + vcol) >> SP2_SH;  // = C[i][col] (tight matched edge)
         const uint32_t cn = (cij == E) ? 0u : (uint32_t)((cij >> 32) + nw1);
         cost += cij;
         dch += child_happy(cn, nw1) - child_happy(co, nw1);

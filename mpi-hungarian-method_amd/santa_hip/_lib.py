@@ -28,6 +28,7 @@ SH_FLAG_VT_TILE = 32
 SH_FLAG_TIMING = 64
 SH_FLAG_SP_TILE = 128
 SH_FLAG_SP1 = 256
+SH_FLAG_TEST_RANGE = 512  # test hook: every register-tile block goes to the fallback launch
 SH_ERRF_ROWS = 1
 SH_ERRF_INFEASIBLE = 2
 SH_ERRF_TYPE = 4
