@@ -286,7 +286,7 @@ def main():
     from santa_hip import _lib
     from santa_hip import data as D
     from santa_hip.context import SantaGPU
-    from santa_hip.driver import World, exchange, shard_range
+    from santa_hip.driver import GPUEngine, World, run_rounds, shard_range
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -303,121 +303,76 @@ def main():
     sd = D.synthetic(args.seed)
     ctx = SantaGPU.from_data(sd, local)
     types = ctx.upload_types(sd.types)
-    backup = torch.empty_like(types)
     _, _, _, nb = ctx.geometry(mode, n)
     b0, b1_, _ = shard_range(nb, rank, world)
     my_blocks = b1_ - b0
     w = World(rank, world, None)
-    buffers = {}
     stream = torch.cuda.current_stream(dev)
-    ev = []  # (start, end) events around the fused block kernel, per timed step
-    state = {"best": None, "score": None}
-    max_rounds = max(args.steps, args.warmup, 1)
-    steps_dev = torch.zeros((max_rounds, max(my_blocks, 1)), dtype=torch.int64, device=dev)
+    max_calls = 2 * max(args.steps, 1) + 2  # (keep-if-improved rounds may be re-run)
+    steps_dev = torch.zeros((max_calls, max(my_blocks, 1)), dtype=torch.int64, device=dev)
 
-    # singles: every round is rescored (as the reference does), but off the
-    # critical path -- the score kernel reads a snapshot of the types on a
-    # side stream while the next round's blocks are solved (always-keep: the
-    # next round does not depend on the score).  Twins keep the synchronous
-    # keep-if-improved decision of mpi_twins.py:166-169.
-    side = torch.cuda.Stream(dev)
-    snaps = [torch.empty_like(types) for _ in range(2)]
-    snap_free = [None, None]
-    sums_dev = torch.zeros((max_rounds, 4), dtype=torch.int64, device=dev)
-    sums_host = torch.zeros((max_rounds, 4), dtype=torch.int64).pin_memory()
-    pending = []
+    class BenchEngine(GPUEngine):
+        """GPUEngine with HIP events (on the launch stream) and the Dijkstra
+        step counts of every timed solve launch."""
 
-    class _Eng:
         def __init__(self, c):
-            self.c = c
+            super().__init__(c)
+            self.timed = False
+            self.ev = []
 
-        def pack_types(self, t, r, o):
-            self.c.pack_types(t, r, o)
-
-        def unpack_types(self, t, r, v, m):
-            self.c.unpack_types(t, r, v, m)
-
-    def step(rnd: int, timed: bool):
-        rows = ctx.sample_blocks(mode, n, nb, args.seed, rnd)
-        if mode != _lib.SH_MODE_SINGLE:
-            backup.copy_(types)
-        if timed:
+        def solve_blocks(self, mode_, rows_, n_, types_):
+            if not self.timed:
+                return self.ctx.solve_blocks(mode_, rows_, n_, types_)
+            k = len(self.ev)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        if my_blocks:
-            # steps per block of the timed launches feed the latency view below
-            ctx.solve_blocks(mode, rows[b0 * n:b1_ * n], n, types,
-                             steps=steps_dev[rnd] if timed else None)
-        if timed:
+            self.ctx.solve_blocks(mode_, rows_, n_, types_, steps=steps_dev[k] if k < max_calls else None)
             e1.record(stream)
-            ev.append((e0, e1))
-        if world > 1:
-            exchange(_Eng(ctx), w, mode, rows, n, nb, types, buffers)
-        if mode == _lib.SH_MODE_SINGLE:
-            k = rnd % 2
-            if snap_free[k] is not None:
-                stream.wait_event(snap_free[k])  # the score of round rnd-2 has read it
-            snaps[k].copy_(types)
-            ready = torch.cuda.Event()
-            ready.record(stream)
-            with torch.cuda.stream(side):
-                side.wait_event(ready)
-                ctx.score_sums_async(snaps[k], out=sums_dev[rnd])
-                sums_host[rnd].copy_(sums_dev[rnd], non_blocking=True)
-                done = torch.cuda.Event()
-                done.record(side)
-            snap_free[k] = done
-            pending.append(rnd)
-            return
-        sc, sg, _, _ = ctx.score_sums(types)  # readback every round, as the reference
-        s = santa_hip.score_from_sums(sc, sg, ctx.nc, ctx.ng, ctx.n_wish, ctx.n_good)
-        if state["best"] is None or s > state["best"]:
-            state["best"] = s
-        else:
-            types.copy_(backup)  # mpi_twins.py:166-169: keep only improvements
-        state["score"] = s
+            self.ev.append((e0, e1))
 
-    def drain():  # host side of the pipelined singles scores (after a device sync)
-        for r in pending:
-            sc, sg = int(sums_host[r, 0]), int(sums_host[r, 1])
-            s = santa_hip.score_from_sums(sc, sg, ctx.nc, ctx.ng, ctx.n_wish, ctx.n_good)
-            if state["best"] is None or s > state["best"]:
-                state["best"] = s
-            state["score"] = s
-        pending.clear()
-
+    eng = BenchEngine(ctx)
     sc0, sg0, _, _ = ctx.score_sums(types)
     score0 = santa_hip.score_from_sums(sc0, sg0, ctx.nc, ctx.ng, ctx.n_wish, ctx.n_good)
+
+    def rounds(k: int):
+        # the reference's round loop (santa_hip.driver.run_rounds), pipelined:
+        # round r's score runs on a side stream from a snapshot while round r+1
+        # is solved (singles keep every round; twins/triplets keep only
+        # improving rounds, speculated and re-run after a rejection); a fixed
+        # number of rounds (no patience stop) so every run times K rounds
+        return run_rounds(eng, types, mode=mode, n=n, seed=args.seed, max_rounds=k, patience=1 << 30,
+                          world=w, score0=score0, pipeline=True)
+
     # warm up on the same rounds, then restart from the baseline assignment so
     # the timed rounds are rounds 0..K-1 of the optimisation (as in the
     # reference, which starts from baseline_res.csv)
-    state["best"] = score0
-    for r in range(args.warmup):
-        step(r % max(args.steps, 1), False)
+    if args.warmup:
+        rounds(args.warmup)
     torch.cuda.synchronize()
-    pending.clear()
     types.copy_(ctx.upload_types(sd.types))
-    state["best"] = score0
     score_start = score0
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    eng.timed = True
     t0 = time.perf_counter()
-    for r in range(args.steps):
-        step(r, True)
+    res = rounds(args.steps)
     torch.cuda.synchronize()
-    drain()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    eng.timed = False
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    ev = eng.ev
+    state = {"best": res.best_score}
+    launches = len(ev)
+    kern_ms = [a.elapsed_time(b) for a, b in ev] or [0.0]
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
     blocks_total = nb * args.steps
     value = blocks_total / elapsed
@@ -434,7 +389,7 @@ def main():
     # alone (same kernel design, untimed region).
     latency = None
     if my_blocks:
-        st = steps_dev[:args.steps, :my_blocks].cpu().numpy().astype(np.int64)
+        st = steps_dev[:min(launches, max_calls), :my_blocks].cpu().numpy().astype(np.int64)
         bmax = int(st[0].argmax())
         rows0 = ctx.sample_blocks(mode, n, nb, args.seed, 0)
         one = rows0[(b0 + bmax) * n:(b0 + bmax + 1) * n].contiguous()
@@ -452,7 +407,7 @@ def main():
         lone_steps = int(s1.item())
         s_per_step = min(lone) / max(lone_steps, 1)
         resident = ctx.resident_blocks(mode, n, my_blocks)
-        chain_floor = float(st.max(axis=1).sum()) * s_per_step          # longest block per round
+        chain_floor = float(st.max(axis=1).sum()) * s_per_step          # longest block per launch
         occ_floor = float(st.sum()) * s_per_step / max(min(resident, my_blocks), 1)
         kern_sum = float(np.sum(kern_ms)) / 1e3
         floor = max(chain_floor, occ_floor)
@@ -462,8 +417,9 @@ def main():
                    "lone_block_steps": lone_steps, "lone_block_ms": round(min(lone) * 1e3, 4),
                    "cycles_per_step_lone": round(s_per_step * CLOCK_HZ, 1),
                    "resident_blocks": resident,
-                   "chain_floor_ms_per_launch": round(chain_floor / args.steps * 1e3, 4),
-                   "occupancy_floor_ms_per_launch": round(occ_floor / args.steps * 1e3, 4),
+                   "launches": launches,
+                   "chain_floor_ms_per_launch": round(chain_floor / max(len(st), 1) * 1e3, 4),
+                   "occupancy_floor_ms_per_launch": round(occ_floor / max(len(st), 1) * 1e3, 4),
                    "binding": "longest block's Dijkstra chain" if chain_floor >= occ_floor else
                               "resident blocks x per-step latency",
                    "frac": round(floor / kern_sum, 4) if kern_sum > 0 else None,

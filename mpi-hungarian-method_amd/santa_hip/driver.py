@@ -17,11 +17,13 @@ Semantics kept from the reference:
     otherwise rolled back (mpi_twins.py:133,166-175); same stop rule;
   * triplets (an extension, accept="improve" as twins): 3-slot units, which
     the reference only asserts (mpi_single.py:32-37).
-Pipelined round (accept="always" on an engine with score_begin): round r's
-score is computed from a snapshot on a side stream while round r+1 is
-sampled and solved; the stop decision of round r is then taken one round
-late and, if it stops the loop, round r+1's speculative update is rolled
-back to round r's snapshot, so results and history equal the serial loop's.
+Pipelined round (an engine with score_begin): round r's score is computed
+from a snapshot on a side stream while round r+1 is sampled and solved from
+round r's result; the decisions of round r are taken one round late: if the
+stop rule fires, round r+1's speculative update is undone; if round r is
+rejected (keep-if-improved), the state returns to round r's starting
+snapshot and round r+1 is run again from it.  Results and history equal the
+serial loop's.
 The reference uses `size` blocks per round (one per MPI rank); the default
 here is every disjoint block of the round ("full"), and
 `blocks_per_round=size` reproduces the reference's schedule.
@@ -131,8 +133,9 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
     check_disjoint: debug mode, assert that each round's blocks are a
     partition (no child in two blocks; twins: no pair overlap), which the
     in-place apply relies on.
-    pipeline: overlap round r's score with round r+1 (accept="always" only,
-    engines with score_begin); identical results and history, but `types`
+    pipeline: overlap round r's score with round r+1 (engines with
+    score_begin; keep-if-improved rounds are speculated and re-run after a
+    rejection); identical results and history, but `types`
     already holds round r+1 when on_round(r) runs, so an on_round that reads
     the state (a checkpoint) needs the serial loop."""
     world = world or World()
@@ -157,9 +160,9 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
     buffers: dict = {}
     backup = torch.empty_like(types) if accept == "improve" else None
     b0, b1, _ = shard_range(B, world.rank, world.size)
-    if pipeline and accept == "always" and hasattr(engine, "score_begin"):
+    if pipeline and hasattr(engine, "score_begin"):
         return _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
-                              on_round, best, check_disjoint, res)
+                              on_round, best, check_disjoint, res, accept)
     for rnd in range(max_rounds):
         t0 = time.perf_counter()
         rows = engine.sample_blocks(mode, n, B, seed, rnd)
@@ -198,52 +201,73 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
 
 
 def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world, on_round, best,
-                   check_disjoint, res: LoopResult) -> LoopResult:
-    """run_rounds for accept="always" with round r's score overlapped with
-    round r+1 (see the module docstring); same decisions and history."""
+                   check_disjoint, res: LoopResult, accept: str = "always") -> LoopResult:
+    """run_rounds with round r's score overlapped with round r+1 (see the
+    module docstring); same decisions, history and final state as the serial
+    loop.  Round r+1 is launched speculatively from round r's result.  When
+    round r turns out rejected (accept="improve": twins, triplets) the state
+    goes back to round r's starting snapshot and round r+1 is run again from
+    it; when the stop rule fires, the speculative round is undone."""
     b0, b1, _ = shard_range(B, world.rank, world.size)
     buffers: dict = {}
+    improve = accept == "improve"
+    pre = [torch.empty_like(types) for _ in range(2)] if improve else None
     count = 0
-    pending = None  # (round, score handle, start time) of the round awaiting its score
+    pending = None  # (round, score handle, start time, pre slot) of the round awaiting its score
     stop = False
     rnd = 0
+
+    def launch(r: int, k: int):
+        if improve:
+            pre[k].copy_(types)  # round r's starting state (its rollback target)
+        rows = engine.sample_blocks(mode, n, B, seed, r)
+        if check_disjoint:
+            assert_disjoint(rows, mode)
+        if b1 > b0:
+            engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types)
+        if world.distributed:
+            exchange(engine, world, mode, rows, n, B, types, buffers)
+        return engine.score_begin(types)
+
     while True:
         if pending is None and (stop or rnd >= max_rounds):
             break
         t0 = time.perf_counter()
         handle = None
+        k = rnd & 1
         if not stop and rnd < max_rounds:
-            rows = engine.sample_blocks(mode, n, B, seed, rnd)
-            if check_disjoint:
-                assert_disjoint(rows, mode)
-            if b1 > b0:
-                engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types)
-            if world.distributed:
-                exchange(engine, world, mode, rows, n, B, types, buffers)
-            handle = engine.score_begin(types)
+            handle = launch(rnd, k)
         if pending is not None:
-            prnd, ph, pt0 = pending
+            prnd, ph, pt0, pk = pending
             sc, sg, bad_tri, bad_tw = ph.result()
             if bad_tri or bad_tw:
                 raise AssertionError("triplets/twins must share a gift (mpi_single.py:32-44)")
             score = engine.score_from_sums(sc, sg)
-            if score > best:
+            improved = score > best
+            if improved:
                 best = score
                 count = 0
             else:
                 count += 1
+            kept = improved or not improve
+            if not kept:
+                types.copy_(pre[pk])  # the state after round prnd is its starting state
             res.rounds += 1
             res.blocks_solved += B
-            st = RoundStats(prnd, sc, sg, score, True, best, B, t0 - pt0)
+            st = RoundStats(prnd, sc, sg, score, kept, best, B, t0 - pt0)
             res.history.append(st)
             if on_round is not None:
                 on_round(st)
             if count > patience:
                 stop = True
-                if handle is not None:  # the serial loop stops here: undo round prnd + 1
-                    ph.restore(types)
+            if handle is not None:
+                if stop:  # the serial loop ends after round prnd: undo the speculative round
+                    if kept:
+                        ph.restore(types)
                     handle = None
-        pending = (rnd, handle, t0) if handle is not None else None
+                elif not kept:  # round rnd ran from a rejected state: run it again
+                    handle = launch(rnd, k)
+        pending = (rnd, handle, t0, k) if handle is not None else None
         rnd += 1
     res.best_score = best
     return res

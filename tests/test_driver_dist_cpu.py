@@ -137,26 +137,45 @@ def test_accept_modes_and_disjoint_check():
         assert_disjoint(torch.tensor([11, 12], dtype=torch.int32), _lib.SH_MODE_TWINS)
 
 
-@pytest.mark.parametrize("patience,rounds", [(-1, 4), (0, 6), (100, 3), (100, 0)])
-def test_pipelined_rounds_equal_serial(patience, rounds):
-    """The pipelined loop (round r's score overlapped with round r+1, a
-    speculative round rolled back when the stop rule fires) makes the same
-    decisions, history and final state as the serial loop."""
+@pytest.mark.parametrize("mode,n,accept,warm", [(0, 64, None, 0), (1, 16, None, 0), (2, 16, None, 0),
+                                                (0, 64, "improve", 0), (1, 16, None, 12), (2, 8, None, 12)])
+@pytest.mark.parametrize("patience,rounds", [(-1, 4), (0, 6), (1, 8), (100, 3), (100, 0)])
+def test_pipelined_rounds_equal_serial(mode, n, accept, warm, patience, rounds):
+    """The pipelined loop (round r's score overlapped with round r+1: a
+    speculative round undone when the stop rule fires, re-run when round r
+    is rejected under keep-if-improved) makes the same decisions, history and
+    final state as the serial loop."""
     from cpu_engine import CPUOracleEngine
     sd = D.synthetic(**SMALL)
+    start = torch.from_numpy(sd.types.copy())
+    if warm:  # a converged state, where keep-if-improved rounds get rejected
+        run_rounds(CPUOracleEngine(sd.wish, sd.goodkids, sd.nq), start, mode=mode, n=n, seed=99,
+                   max_rounds=warm, patience=100, world=World())
     out = []
+    seen = []
     for pipeline in (False, True):
         eng = CPUOracleEngine(sd.wish, sd.goodkids, sd.nq)
-        t = torch.from_numpy(sd.types.copy())
-        res = run_rounds(eng, t, mode=_lib.SH_MODE_SINGLE, n=64, seed=5, max_rounds=rounds,
+        t = start.clone()
+        res = run_rounds(eng, t, mode=mode, n=n, seed=5, max_rounds=rounds, accept=accept,
                          patience=patience, world=World(), pipeline=pipeline)
         hist = [(st.round, st.s_child, st.s_gift, st.score, st.accepted, st.best) for st in res.history]
+        seen.append(any(not st.accepted for st in res.history))
         out.append((t.numpy().copy(), hist, res.rounds, res.blocks_solved, res.best_score))
     (t0, h0, r0, b0, s0), (t1, h1, r1, b1, s1) = out
     assert np.array_equal(t0, t1)
     assert h0 == h1 and r0 == r1 and b0 == b1 and s0 == s1
     if patience == -1:
         assert r0 == 1  # stopped after the first round; the speculative second was undone
+    rejected_rounds_seen.append(seen[0])
+
+
+rejected_rounds_seen = []
+
+
+def test_pipelined_rejections_were_exercised():
+    """(the keep-if-improved cases above must include rejected rounds, so the
+    re-run path of the pipelined loop was compared with the serial loop)"""
+    assert any(rejected_rounds_seen)
 
 
 def test_triplet_rounds_keep_units():
