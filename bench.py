@@ -463,7 +463,7 @@ def main():
                      "algorithmic_bytes_per_block": per_block, "latency": latency},
         "cpu": cpu,
     }
-    if mode == 0 and world == 1:  # the PMC passes profile a full one-GPU round
+    if world == 1:  # the PMC passes profile a full one-GPU round (tools/profile_round.sh)
         out["roofline"].update(stored_traffic(design_kernels(kname)))
     if want_cpu:
         cb = cpu_baseline(sd, mode, n, args.cpu_seconds, cpu["used"])
