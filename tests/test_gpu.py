@@ -705,3 +705,41 @@ def test_context_on_a_second_device(sh, full_data):
     oracle.round_blocks(0, full_data.wish, t_host, rows.cpu().numpy().reshape(8, 256), ng=full_data.ng)
     assert np.array_equal(types.cpu().numpy(), t_host)
     assert c1.error_flags() == 0
+
+
+# --------------------------------------------------------------------------- CLI end to end
+@pytest.mark.parametrize("mode", ["single", "twins", "triplets"])
+def test_cli_rounds_end_to_end(sh, full_data, mode, tmp_path, capsys):
+    """`python -m santa_hip.driver` (the reference scripts' entry, no
+    arguments there): seeded synthetic data, a few rounds, the per-round
+    checkpoint and the final CSV.  The final CSV keeps every family on one
+    gift and every gift type at its quantity; its score is the printed best;
+    the pipelined and serial loops write byte-identical files."""
+    import json
+
+    import oracle
+    from santa_hip import data as D
+    from santa_hip.driver import main
+    outs = []
+    for extra in ([], ["--no-pipeline"]):
+        p = tmp_path / f"sub_{len(outs)}.csv"
+        assert main(["--mode", mode, "--block-size", "128", "--rounds", "3", "--out", str(p),
+                     "--check-disjoint", "--seed", "5"] + extra) == 0
+        lines = [json.loads(x) for x in capsys.readouterr().out.strip().splitlines()]
+        outs.append((p.read_bytes(), lines))
+    assert outs[0][0] == outs[1][0]
+    assert [x.get("score") for x in outs[0][1]] == [x.get("score") for x in outs[1][1]]
+    t = D.read_submission(str(tmp_path / "sub_0.csv"), full_data.nc, full_data.ng)
+    assert np.array_equal(np.bincount(t, minlength=full_data.ng), np.bincount(full_data.types, minlength=full_data.ng))
+    sc, sg, bt, btw = oracle.score_sums(full_data.wish, full_data.goodkids, t)
+    assert bt == 0 and btw == 0
+    s = oracle.score_from_sums(sc, sg, full_data.nc, full_data.ng, full_data.n_wish, full_data.n_good)
+    # singles keep every round (the last round's state); twins/triplets the best one
+    want = outs[0][1][-2]["score"] if mode == "single" else outs[0][1][-1]["best_score"]
+    assert s == want
+    # --checkpoint-every rewrites --out after each round (the reference's to_csv per round)
+    p = tmp_path / "ck.csv"
+    assert main(["--mode", mode, "--block-size", "128", "--rounds", "2", "--out", str(p),
+                 "--checkpoint-every", "1", "--seed", "5"]) == 0
+    capsys.readouterr()
+    assert p.exists() and p.stat().st_size > 0
