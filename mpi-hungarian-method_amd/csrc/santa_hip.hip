@@ -2360,7 +2360,7 @@ __device__ __forceinline__ uint32_t tile_entry(uint32_t h) {
 // are allocated from one LDS counter (a block fits iff its total overflow
 // does, whatever the order the waves allocate in).
 template <bool VEC>
-__global__ __launch_bounds__(TILE_NW * WAVE) void santa_tile_kernel(SantaArgs a, unsigned char *rec_all) {
+__global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(4))) void santa_tile_kernel(SantaArgs a, unsigned char *rec_all) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2491,7 +2491,6 @@ __global__ __launch_bounds__(TILE_NW * WAVE) void santa_tile_kernel(SantaArgs a,
   for (int s0 = r0w; s0 < rend; s0 += RPS) {
     const int row = s0 + qr;
     const bool lr = row < n;
-    const int mt = mtn;
     uint2 q[MAXQ];
 #pragma unroll
     for (int t = 0; t < MAXQ; ++t) q[t] = qn[t];
@@ -2502,17 +2501,18 @@ __global__ __launch_bounds__(TILE_NW * WAVE) void santa_tile_kernel(SantaArgs a,
     }
     uint32_t hv[MAXQ][4];
     int cnt = 0;
-    uint32_t ownc = 0;
 #pragma unroll
     for (int t = 0; t < MAXQ; ++t) {
 #pragma unroll
       for (int z = 0; z < 4; ++z) {
         const int g = gift_of(q[t], z);
-        const bool ok = lr && (t < ncq) && (cb + t < nch) && (g >= 0);
-        const uint32_t h = thead[ok ? g : 0];
+        // (VEC: every loaded gift is a valid type -- the context validates the
+        // wishlists and the chunk index is clamped -- so the table read needs no
+        // guard; the non-VEC path pads with -1)
+        const bool ok = lr && (t < ncq) && (cb + t < nch) && (VEC || g >= 0);
+        const uint32_t h = thead[VEC ? g : (ok ? g : 0)];
         hv[t][z] = ok ? h : 0u;
         cnt += (int)(hv[t][z] >> 24);
-        ownc = (ok && g == mt) ? (uint32_t)(4 * (cb + t) + z + 1) : ownc;
       }
     }
     const uint32_t incl = wave_incl_scan_u32((uint32_t)cnt);
@@ -2524,7 +2524,6 @@ __global__ __launch_bounds__(TILE_NW * WAVE) void santa_tile_kernel(SantaArgs a,
     const int start = (int)incl - cnt;
     if (qj == 0) off_l[qr] = (uint16_t)start;
     if (lane == 0) off_l[RPS] = (uint16_t)total;
-    if (ownc) own[row] = (uint8_t)ownc;
     int p = start;
     bool many = false;
 #pragma unroll
@@ -2565,10 +2564,14 @@ __global__ __launch_bounds__(TILE_NW * WAVE) void santa_tile_kernel(SantaArgs a,
         const int o0 = off_l[rl];
         const int cr = (s0 + rl < n) ? (int)off_l[rl + 1] - o0 : 0;
         uint32_t e = 256u + (uint32_t)x31;  // unused entry: the lane's dump slot
-        if (cr > 32 && x31 == 31)
+        if (cr > 32 && x31 == 31) {
           e = (256u + 31u) | (SP2_MARK << 9);
-        else if (x31 < cr)
+        } else if (x31 < cr) {
           e = tile_entry(hits[o0 + x31]);
+          // the row's own column (the old gift's code, for the deltas): the
+          // entry whose slot is that of column s0 + rl (at most one per row)
+          if ((e & 0xFFu) == (uint32_t)rowc_slot(s0 + rl)) own[s0 + rl] = (uint8_t)(nw + 1 - (e >> 9));
+        }
         w |= e << (16 * H);
       }
       rtile[tile_word((s0 >> 2) + qq, lane)] = w;
@@ -2587,7 +2590,11 @@ __global__ __launch_bounds__(TILE_NW * WAVE) void santa_tile_kernel(SantaArgs a,
           fits = false;
           break;
         }
-        for (int x = lane; x < extra; x += WAVE) rovf[obase + x] = (uint16_t)tile_entry(hits[o0 + 31 + x]);
+        for (int x = lane; x < extra; x += WAVE) {
+          const uint32_t e = tile_entry(hits[o0 + 31 + x]);
+          rovf[obase + x] = (uint16_t)e;
+          if ((e & 0xFFu) == (uint32_t)rowc_slot(s0 + rl)) own[s0 + rl] = (uint8_t)(nw + 1 - (e >> 9));
+        }
         if (lane == 0) rovfr[s0 + rl] = (uint32_t)obase | ((uint32_t)extra << 16);
       }
     }
