@@ -209,3 +209,26 @@ def test_lsap_front_end_routes_wide_integers_to_float64(monkeypatch):
     lsap.linear_sum_assignment(np.array([[1, 2], [3, 4]], dtype=np.uint8), maximize=True, device="cpu")
     lsap.linear_sum_assignment(np.array([[0.5, 2], [3, 4]]), device="cpu")
     assert seen == [torch.int64, torch.float64, torch.int64, torch.float64]
+
+
+def test_bench_roofline_helpers():
+    """bench.py's roofline plumbing on the CPU: the register-tile design's
+    launch is two kernels (tile build + solve), and the stored HBM traffic
+    comes only from a committed rocprofv3 summary of the same kernel source
+    (otherwise null with a note naming the source hash)."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.design_kernels("santa_sp2_kernel (1-wave sparse register tile)") == \
+        ["santa_tile_kernel", "santa_sp2_kernel"]
+    assert bench.design_kernels("santa_block_kernel (twins, 4-wave code-pair tile)") == ["santa_block_kernel"]
+    t = bench.stored_traffic(["santa_tile_kernel", "santa_sp2_kernel"])
+    if t["traffic"] is None:
+        assert "kernel source" in t["traffic_note"]
+    else:
+        raw = t["traffic_raw"]
+        assert t["traffic"] == round(raw["FETCH_SIZE"] * raw["fetch_correction"] + raw["WRITE_SIZE"])
+        assert raw["kernels"] == ["santa_tile_kernel", "santa_sp2_kernel"]
