@@ -68,6 +68,10 @@ extern "C" {
                                    treats every block as outside its
                                    scaled-unit range, so all blocks take the
                                    fallback launch (same results)          */
+#define SH_FLAG_NO_APPLY 1024u  /* solve and report (col, cost, deltas,
+                                   steps) but leave the gift types untouched:
+                                   blocks may then overlap (batched
+                                   measurements of independent blocks)     */
 
 /* Kernel designs sh_solve_blocks can dispatch to (sh_solve_design).        */
 #define SH_DESIGN_SPARSE 0   /* one wave per block, hit lists in LDS        */

@@ -909,8 +909,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   // every old type into ctype before this point, so in-place is race-free.
   for (int i = tid; i < n; i += SANTA_WG) {
     const int16_t tnew = ctype[S.c4r[i]];
-    a.types[rows_l[i]] = tnew;
-    if (MODE) a.types[rows_l[i] + 1] = tnew;
+    if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[rows_l[i]] = tnew;
+    if (MODE && !(a.flags & SH_FLAG_NO_APPLY)) a.types[rows_l[i] + 1] = tnew;
   }
   __syncthreads();
   if (tid == 0) {
@@ -1328,8 +1328,8 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
     const int col = c4r_l[j];  // here j plays the row
     if (a.col) a.col[(size_t)b * n + j] = col;
     const int16_t tnew = ctype[col];
-    a.types[rows_l[j]] = tnew;
-    if (MODE) a.types[rows_l[j] + 1] = tnew;
+    if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[rows_l[j]] = tnew;
+    if (MODE && !(a.flags & SH_FLAG_NO_APPLY)) a.types[rows_l[j] + 1] = tnew;
   }
   __syncthreads();
   if (tid == 0) {
@@ -1675,7 +1675,7 @@ __global__ __launch_bounds__(WAVE, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
         if (a.delta) dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
       }
       if (a.col) a.col[(size_t)b * n + i] = col;
-      a.types[child] = (int16_t)tnew;  // this block owns child; ctype holds old types
+      if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[child] = (int16_t)tnew;  // this block owns child; ctype holds old types
     }
   }
   cost = wave_sum_i64(cost);
@@ -2264,7 +2264,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
         if (a.delta) dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
       }
       if (a.col) a.col[(size_t)b * n + i] = col;
-      a.types[child] = (int16_t)tnew;  // this block owns child; ctype holds old types
+      if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[child] = (int16_t)tnew;  // this block owns child; ctype holds old types
     }
   }
   cost = wave_sum_i64(cost);
@@ -2931,7 +2931,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         if (a.delta) dgh += gift_happy(a, chd, tnew) - gift_happy(a, chd, told);
       }
       if (a.col) a.col[(size_t)b * n + i] = col;
-      a.types[chd] = (int16_t)tnew;  // this block owns chd; ctype holds old types
+      if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[chd] = (int16_t)tnew;  // this block owns chd; ctype holds old types
     }
   }
   cost = wave_sum_i64(cost);
@@ -3179,7 +3179,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
   __syncthreads();  // every old type was read from ctype (LDS): apply in place
   for (int i = tid; i < n; i += WG) {
     const int16_t tnew = ctype[S.c4r[i]];
-    for (int m = 0; m <= MODE; ++m) a.types[rows_l[i] + m] = tnew;
+    if (!(a.flags & SH_FLAG_NO_APPLY)) for (int m = 0; m <= MODE; ++m) a.types[rows_l[i] + m] = tnew;
   }
   if (tid == 0) {
     int64_t tc = 0, t0 = 0, t1 = 0;

@@ -29,6 +29,7 @@ SH_FLAG_TIMING = 64
 SH_FLAG_SP_TILE = 128
 SH_FLAG_SP1 = 256
 SH_FLAG_TEST_RANGE = 512  # test hook: every register-tile block goes to the fallback launch
+SH_FLAG_NO_APPLY = 1024  # solve without writing the gift types (overlapping blocks allowed)
 SH_ERRF_ROWS = 1
 SH_ERRF_INFEASIBLE = 2
 SH_ERRF_TYPE = 4

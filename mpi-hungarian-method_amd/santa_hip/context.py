@@ -118,7 +118,8 @@ class SantaGPU:
                      col: torch.Tensor | None = None, cost: torch.Tensor | None = None,
                      delta: torch.Tensor | None = None, steps: torch.Tensor | None = None,
                      flags: int = 0) -> None:
-        """Build, solve and apply B = rows.numel() // n disjoint blocks in place."""
+        """Build, solve and apply B = rows.numel() // n disjoint blocks in place
+        (with SH_FLAG_NO_APPLY: solve only, types untouched, blocks may overlap)."""
         assert rows.dtype == torch.int32 and rows.is_contiguous() and rows.device == self.device
         assert types.dtype == torch.int16 and types.numel() == self.nc and types.device == self.device
         B = rows.numel() // n

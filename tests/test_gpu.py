@@ -743,3 +743,33 @@ def test_cli_rounds_end_to_end(sh, full_data, mode, tmp_path, capsys):
                  "--checkpoint-every", "1", "--seed", "5"]) == 0
     capsys.readouterr()
     assert p.exists() and p.stat().st_size > 0
+
+
+def test_no_apply_solves_overlapping_blocks(sh, ctx, full_data):
+    """SH_FLAG_NO_APPLY: blocks are solved and reported (col, cost) but the
+    gift types stay untouched, so overlapping blocks (the same block twice,
+    blocks of two samplings) each equal the oracle's solve from the initial
+    state; every design honours it."""
+    from santa_hip import _lib
+    n = 256
+    r0 = ctx.sample_blocks(0, n, 6, 3, 0)
+    r1 = ctx.sample_blocks(0, n, 6, 3, 1)
+    rows = torch.cat([r0, r1, r0[:n]])  # overlapping blocks
+    B = rows.numel() // n
+    r = rows.cpu().numpy().reshape(B, n)
+    want = []
+    for b in range(B):
+        C = oracle.cost_single(full_data.wish, full_data.types, r[b], ng=full_data.ng)
+        _, oc = oracle.lsap(C)
+        want.append((oc, int(C[np.arange(n), oc].sum())))
+    for fl in (0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1, _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_VT_TILE,
+               _lib.SH_FLAG_SW_TILE):
+        types = ctx.upload_types(full_data.types)
+        col = torch.empty(B * n, dtype=torch.int32, device="cuda")
+        cost = torch.empty(B, dtype=torch.int64, device="cuda")
+        ctx.solve_blocks(0, rows, n, types, col=col, cost=cost, flags=fl | _lib.SH_FLAG_NO_APPLY)
+        assert np.array_equal(types.cpu().numpy(), full_data.types), fl
+        c = col.cpu().numpy().reshape(B, n)
+        for b in range(B):
+            assert np.array_equal(c[b], want[b][0]) and int(cost[b]) == want[b][1], (fl, b)
+    assert ctx.error_flags() == 0
