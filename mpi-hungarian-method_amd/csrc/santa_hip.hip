@@ -2315,7 +2315,6 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
 // A Dijkstra step reads its row with one indexed VGPR move (s_set_gpr_idx)
 // instead of a range lookup and an LDS read.
 // ---------------------------------------------------------------------------
-constexpr int SP2_SUB_CAP = 512;   // hit entries of one 8-row build sub-round
 constexpr uint32_t SP2_MARK = 127; // overflow marker in the `a` field (n_wish <= 126)
 constexpr int SP2_OVF_CAP = 512;   // overflow entries per block
 // per-block record in HBM (bytes): tile | ovf | ovfr | own | status
@@ -2326,10 +2325,11 @@ constexpr size_t SP2_REC_OWN = SP2_REC_OVFR + 256 * 4;
 constexpr size_t SP2_REC_STATUS = SP2_REC_OWN + 256;
 constexpr size_t SP2_REC = SP2_REC_STATUS + 128;  // 18816 bytes
 
-constexpr int TILE_NW = 4;  // waves per block of the tile build (64 rows each)
+constexpr int TILE_NW = 4;  // waves per block of the tile build (one row per thread)
+constexpr int TILE_RS = 17; // staging row stride in dwords (32 entries + pad: conflict-free rows)
 
 struct TileLds {
-  size_t own, csort, thead, ocnt, off, hits, total;
+  size_t own, csort, thead, ocnt, rcnt, stage, total;
 };
 
 __host__ __device__ __forceinline__ TileLds tile_lds_layout(int ng) {
@@ -2338,27 +2338,24 @@ __host__ __device__ __forceinline__ TileLds tile_lds_layout(int ng) {
   L.own = o;    o += 256;                      // code(i, i): row i's own (old) gift
   L.csort = o;  o += 272;                      // columns sorted by gift type (+ pad)
   L.thead = o;  o += r16((size_t)ng * 4);      // counting-sort counters, then the type table
-  L.ocnt = o;   o += 16;                       // overflow entries allocated (all waves)
-  L.off = o;    o += TILE_NW * 32;             // per wave: hit-list offsets of its sub-round's 8 rows
-  L.hits = o;   o += TILE_NW * (SP2_SUB_CAP + 2 * 64) * 2;  // per wave: the sub-round's list + dumps
+  L.ocnt = o;   o += 16;                       // overflow entries allocated (all rows)
+  L.rcnt = o;   o += 256;                      // per row: tile entries used (<= 32), | 0x80 = marker
+  L.stage = o;  o += (size_t)256 * TILE_RS * 4;  // per row: its tile entries (uint16), row-major
   L.total = o;
   return L;
 }
 
-// dword index of (VGPR q, lane) in a tile record: 4 consecutive VGPRs of a
-// lane are one 16-byte word, lanes contiguous (coalesced 16-byte loads)
-__device__ __forceinline__ int tile_word(int q, int lane) { return ((q >> 2) * 64 + lane) * 4 + (q & 3); }
-
-// hit-list entry of the build (slot | (code - nw1) << 8) -> tile entry (slot | a << 9)
-__device__ __forceinline__ uint32_t tile_entry(uint32_t h) {
-  return (h & 0xFFu) | ((uint32_t)(-(int)(int8_t)(h >> 8)) << 9);
-}
-
-// Four waves per block: the column sort is shared, then wave w builds rows
-// 64w..64w+63 (8 sub-rounds of 8 rows) with its own LDS list, so a block's
-// 32 dependent wishlist-load rounds run as 4 chains of 8.  Overflow entries
-// are allocated from one LDS counter (a block fits iff its total overflow
-// does, whatever the order the waves allocate in).
+// Row-owner build: the column sort is shared (as santa_sp_kernel), then thread
+// i owns row i: it loads its child's whole wishlist into registers (one round
+// of loads), counts the row's hits with one type-table read per wish (pass 1:
+// the count decides the overflow split and allocates the row's overflow range
+// from one LDS counter -- a block fits iff its total overflow does), and
+// emits them in wish order (pass 2: the same order as santa_sp_kernel's hit
+// lists) into a row-major LDS staging area, spilling entries 31.. of a row
+// with more than 32 hits to the overflow list.  The staging area is then
+// transposed into the record's VGPR layout with coalesced 16-byte stores.
+// (Round 2's first version built 8 rows per sub-round with 8 lanes per row
+// and a wave scan: ~8,500 instructions per wave against ~3,000 here.)
 template <bool VEC>
 __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(4))) void santa_tile_kernel(SantaArgs a, unsigned char *rec_all) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2371,13 +2368,14 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
   uint32_t *thead = (uint32_t *)(smem + L.thead);
   uint32_t *tcnt = thead;  // counting-sort counters, turned into the type table in place
   int32_t *ocnt = (int32_t *)(smem + L.ocnt);
-  uint16_t *off_l = (uint16_t *)(smem + L.off) + wv * 16;
-  uint16_t *hits = (uint16_t *)(smem + L.hits) + wv * (SP2_SUB_CAP + 2 * 64);
+  uint8_t *rcnt = smem + L.rcnt;
+  uint16_t *stage = (uint16_t *)(smem + L.stage);
   unsigned char *rec = rec_all + (size_t)b * SP2_REC;
   uint32_t *rtile = (uint32_t *)(rec + SP2_REC_TILE);
   uint16_t *rovf = (uint16_t *)(rec + SP2_REC_OVF);
   uint32_t *rovfr = (uint32_t *)(rec + SP2_REC_OVFR);
   int32_t *status = (int32_t *)(rec + SP2_REC_STATUS);
+  (void)wv;
 
   // -- rows (thread t owns row t), range check ----------------------------------------
   const bool live = tid < n;
@@ -2388,6 +2386,40 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
       *status = 1;  // skip
     }
     return;
+  }
+  // the row's wishlist into registers: two gifts per dword (one round of loads,
+  // in flight during the column sort)
+  const int nw = a.n_wish;
+  const int ndw = (nw + 1) >> 1;
+  u32x32 G0, G1;
+  {
+    const int16_t *src = a.wish + (size_t)child * nw;
+    if constexpr (VEC) {  // n_wish % 4 == 0: 8-byte chunks
+      const uint2 *s2 = (const uint2 *)src;
+      const int nch = nw >> 2;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const uint2 v = (live && c < nch) ? s2[c] : make_uint2(0, 0);
+        G0[2 * c] = v.x;
+        G0[2 * c + 1] = v.y;
+      }
+#pragma unroll
+      for (int c = 16; c < 32; ++c) {
+        const uint2 v = (live && c < nch) ? s2[c] : make_uint2(0, 0);
+        G1[2 * c - 32] = v.x;
+        G1[2 * c - 31] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < 64; ++d) {
+        const uint32_t lo = (live && 2 * d < nw) ? (uint16_t)src[2 * d] : 0u;
+        const uint32_t hi = (live && 2 * d + 1 < nw) ? (uint16_t)src[2 * d + 1] : 0u;
+        if (d < 32)
+          G0[d] = lo | (hi << 16);
+        else
+          G1[d - 32] = lo | (hi << 16);
+      }
+    }
   }
   // -- columns sorted by gift type (counting sort, as santa_sp_kernel) ---------------
   for (int t = tid; t < a.ng; t += TILE_NW * WAVE) tcnt[t] = 0u;
@@ -2405,7 +2437,7 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
   if (myt >= 0) atomicAdd(&tcnt[myt], 1u << 16);
   __syncthreads();
   int big = 0;
-  if (wv == 0) {  // exclusive scan of the counts over types -> start of each type in csort
+  if (tid < WAVE) {  // exclusive scan of the counts over types -> start of each type in csort
     const int per = (a.ng + WAVE - 1) / WAVE;
     const int t0s = lane * per, t1s = min(a.ng, t0s + per);
     uint32_t sum = 0;
@@ -2438,167 +2470,90 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
   }
   __syncthreads();
 
-  // -- the tile, 8 rows per sub-round, 8 lanes per row -------------------------------
-  // As santa_sp_kernel: lane 8q+j takes wishlist chunks [j*ncq, (j+1)*ncq) of row
-  // s0+q, looks them up in the type table, and one wave scan places the hits in
-  // the sub-round's LDS list (rows in order).  The list then goes to the tile:
-  // lane 32L+x takes entry x of the two rows of each VGPR it holds.
-  const int nw = a.n_wish;
-  constexpr int LPR = 8;                         // lanes per row
-  constexpr int RPS = WAVE / LPR;                // rows per sub-round
-  constexpr int MAXQ = 4;                        // chunks per lane (n_wish <= 127)
-  const int nch = (nw + 3) >> 2;
-  const int ncq = (nch + LPR - 1) / LPR;
-  const int qr = lane / LPR, qj = lane % LPR;
+  // -- pass 1: the row's hit count and its own gift's code -----------------------------
+  // (gifts four at a time: dwords d, d + 1 of the register copy, four type-table
+  // reads in flight; r >= n_wish pads read type 0 and are masked out)
+  auto gifts4 = [&](int d, int (&g)[4]) {
+    const uint32_t w0 = (d < 32) ? G0[d] : G1[d - 32];
+    const uint32_t w1 = (d + 1 < 32) ? G0[d + 1] : G1[d - 31];
+    g[0] = (int)(w0 & 0xFFFFu);
+    g[1] = (int)(w0 >> 16);
+    g[2] = (int)(w1 & 0xFFFFu);
+    g[3] = (int)(w1 >> 16);
+  };
   bool fits = true;
-  auto load_chunk = [&](const int16_t *src, int c) -> uint2 {
-    uint2 q;
-    if constexpr (VEC) {
-      q = *(const uint2 *)(src + 4 * min(c, nch - 1));
-    } else {
-      uint32_t g4[4];
-#pragma unroll
-      for (int z = 0; z < 4; ++z) {
-        const int r = 4 * c + z;
-        g4[z] = (r < nw) ? (uint16_t)src[min(r, nw - 1)] : 0xFFFFu;
-      }
-      q.x = g4[0] | (g4[1] << 16);
-      q.y = g4[2] | (g4[3] << 16);
-    }
-    return q;
-  };
-  auto gift_of = [](const uint2 &q, int z) -> int {
-    return (int)(int16_t)(((z < 2 ? q.x : q.y) >> (16 * (z & 1))) & 0xFFFFu);
-  };
-  const int dump = SP2_SUB_CAP + 2 * lane;
-  const int cb = qj * ncq;
-  // child id | (own type + 1) << 20 of this wave's rows (children < 2^20, types < 1023)
-  const int ct = child | ((myt + 1) << 20);
-  auto row_child = [&](int rloc, int &chd, int &mt) {  // rloc: row within the wave's 64
-    const int x = __shfl(ct, rloc & 63, WAVE);
-    chd = x & 0xFFFFF;
-    mt = (x >> 20) - 1;
-  };
-  const int r0w = WAVE * wv;  // the wave's first row
-  const int rend = min(n, r0w + WAVE);
-  const int Lh = lane >> 5, x31 = lane & 31;
-  uint2 qn[MAXQ];
-  int chdn, mtn;
-  row_child(qr, chdn, mtn);
-#pragma unroll
-  for (int t = 0; t < MAXQ; ++t) qn[t] = load_chunk(a.wish + (size_t)chdn * nw, cb + t);
+  int lim = 32, obase = 0;
+  if (live) {
+    uint32_t total = 0;
+    int ownc = 0;
 #pragma unroll 1
-  for (int s0 = r0w; s0 < rend; s0 += RPS) {
-    const int row = s0 + qr;
-    const bool lr = row < n;
-    uint2 q[MAXQ];
+    for (int d = 0; d < ndw; d += 2) {
+      int g[4];
+      gifts4(d, g);
+      uint32_t h[4];
 #pragma unroll
-    for (int t = 0; t < MAXQ; ++t) q[t] = qn[t];
-    if (s0 + RPS < rend) {
-      row_child(s0 + RPS - r0w + qr, chdn, mtn);
-#pragma unroll
-      for (int t = 0; t < MAXQ; ++t) qn[t] = load_chunk(a.wish + (size_t)chdn * nw, cb + t);
-    }
-    uint32_t hv[MAXQ][4];
-    int cnt = 0;
-#pragma unroll
-    for (int t = 0; t < MAXQ; ++t) {
+      for (int z = 0; z < 4; ++z) h[z] = thead[(VEC || 2 * d + z < nw) ? g[z] : 0];
 #pragma unroll
       for (int z = 0; z < 4; ++z) {
-        const int g = gift_of(q[t], z);
-        // (VEC: every loaded gift is a valid type -- the context validates the
-        // wishlists and the chunk index is clamped -- so the table read needs no
-        // guard; the non-VEC path pads with -1)
-        const bool ok = lr && (t < ncq) && (cb + t < nch) && (VEC || g >= 0);
-        const uint32_t h = thead[VEC ? g : (ok ? g : 0)];
-        hv[t][z] = ok ? h : 0u;
-        cnt += (int)(hv[t][z] >> 24);
-      }
-    }
-    const uint32_t incl = wave_incl_scan_u32((uint32_t)cnt);
-    const int total = __builtin_amdgcn_readlane((int)incl, 63);
-    if (total > SP2_SUB_CAP) {
-      fits = false;
-      break;
-    }
-    const int start = (int)incl - cnt;
-    if (qj == 0) off_l[qr] = (uint16_t)start;
-    if (lane == 0) off_l[RPS] = (uint16_t)total;
-    int p = start;
-    bool many = false;
-#pragma unroll
-    for (int t = 0; t < MAXQ; ++t)
-#pragma unroll
-      for (int z = 0; z < 4; ++z) {
-        const uint32_t h = hv[t][z];
-        const int cg = (int)(h >> 24);
-        const uint32_t tb = ((uint32_t)(4 * (cb + t) + z - nw) & 0xFFu) << 8;
-        hits[cg >= 1 ? p : dump] = (uint16_t)(tb | (h & 0xFFu));
-        hits[cg >= 2 ? p + 1 : dump] = (uint16_t)(tb | ((h >> 8) & 0xFFu));
-        hits[cg == 3 ? p + 2 : dump] = (uint16_t)(tb | ((h >> 16) & 0xFFu));
-        many |= cg >= 4;
-        p += cg;
-      }
-    if (__builtin_expect(__any(many), 0)) {  // types with 4+ columns in this block
-      int pp = start;
-#pragma unroll
-      for (int t = 0; t < MAXQ; ++t)
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-          const int cg = (int)(hv[t][z] >> 24);
-          const int e = (int)((hv[t][z] >> 16) & 0xFFu);  // start in csort when cg >= 4
-          const uint32_t tb = ((uint32_t)(4 * (cb + t) + z - nw) & 0xFFu) << 8;
-          if (cg >= 4)
-            for (int x = 2; x < cg; ++x) hits[pp + x] = (uint16_t)(tb | csort[e + x]);
-          pp += cg;
+        const int r = 2 * d + z;
+        if (VEC || r < nw) {  // (uniform)
+          total += h[z] >> 24;
+          ownc = (g[z] == myt) ? r + 1 : ownc;  // (the last occurrence, as the reference's overwrite)
         }
-    }
-    // -- the 8 rows' lists into the tile record (VGPRs s0/4 and s0/4 + 1) ------
-    // (the wave's LDS accesses are in order: the reads below see the writes)
-#pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-      uint32_t w = 0;
-#pragma unroll
-      for (int H = 0; H < 2; ++H) {
-        const int rl = 4 * qq + 2 * Lh + H;  // local row of this lane's half
-        const int o0 = off_l[rl];
-        const int cr = (s0 + rl < n) ? (int)off_l[rl + 1] - o0 : 0;
-        uint32_t e = 256u + (uint32_t)x31;  // unused entry: the lane's dump slot
-        if (cr > 32 && x31 == 31) {
-          e = (256u + 31u) | (SP2_MARK << 9);
-        } else if (x31 < cr) {
-          e = tile_entry(hits[o0 + x31]);
-          // the row's own column (the old gift's code, for the deltas): the
-          // entry whose slot is that of column s0 + rl (at most one per row)
-          if ((e & 0xFFu) == (uint32_t)rowc_slot(s0 + rl)) own[s0 + rl] = (uint8_t)(nw + 1 - (e >> 9));
-        }
-        w |= e << (16 * H);
       }
-      rtile[tile_word((s0 >> 2) + qq, lane)] = w;
     }
-    // rows with more than 32 hits: entries 31.. to the overflow list
+    own[tid] = (uint8_t)ownc;
+    if (total > 32u) {  // entries 31.. to the overflow list, the marker in entry 31
+      lim = 31;
+      const int extra = (int)total - 31;
+      obase = atomicAdd(ocnt, extra);
+      if (obase + extra > a.cap) fits = false;  // a.cap <= SP2_OVF_CAP (tests lower it)
+      else rovfr[tid] = (uint32_t)obase | ((uint32_t)extra << 16);
+    }
+    rcnt[tid] = (uint8_t)(total > 32u ? 0x80u | 31u : total);
+  }
+  // -- pass 2: the entries (slot | a << 9, a = n_wish - rank) in wish order -------------
+  // Branch-free for a type's first two columns (a write per column slot, to the
+  // row's pad entry 32 when the type has fewer columns or the entry overflows);
+  // third and further columns and overflow entries behind wave-uniform tests.
+  if (live && fits) {
+    uint16_t *srow = stage + tid * (2 * TILE_RS);
+    uint16_t *orow = rovf + obase - lim;  // entry x >= lim goes to orow[x]
+    int x = 0;
 #pragma unroll 1
-    for (int rl = 0; rl < RPS && s0 + rl < n; ++rl) {
-      const int o0 = off_l[rl];
-      const int cr = (int)off_l[rl + 1] - o0;
-      if (cr > 32) {
-        const int extra = cr - 31;
-        int obase = 0;
-        if (lane == 0) obase = atomicAdd(ocnt, extra);
-        obase = __builtin_amdgcn_readfirstlane(obase);
-        if (obase + extra > a.cap) {  // a.cap <= SP2_OVF_CAP (tests lower it)
-          fits = false;
-          break;
+    for (int d = 0; d < ndw; d += 2) {
+      int g[4];
+      gifts4(d, g);
+      uint32_t h[4];
+#pragma unroll
+      for (int z = 0; z < 4; ++z) h[z] = thead[(VEC || 2 * d + z < nw) ? g[z] : 0];
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int r = 2 * d + z;
+        if (!(VEC || r < nw)) continue;  // (uniform)
+        const uint32_t hz = h[z];
+        const uint32_t A = (uint32_t)(nw - r) << 9;
+        const int cg = (int)(hz >> 24);
+        srow[(cg >= 1 && x < lim) ? x : 32] = (uint16_t)((hz & 0xFFu) | A);
+        srow[(cg >= 2 && x + 1 < lim) ? x + 1 : 32] = (uint16_t)(((hz >> 8) & 0xFFu) | A);
+        if (__any(cg >= 3)) {
+          if (cg == 3) {
+            srow[x + 2 < lim ? x + 2 : 32] = (uint16_t)(((hz >> 16) & 0xFFu) | A);
+          } else if (cg >= 4) {  // the type's columns 2.. from csort
+            const int e = (int)((hz >> 16) & 0xFFu);
+            for (int m = 2; m < cg; ++m) srow[x + m < lim ? x + m : 32] = (uint16_t)((uint32_t)csort[e + m] | A);
+          }
         }
-        for (int x = lane; x < extra; x += WAVE) {
-          const uint32_t e = tile_entry(hits[o0 + 31 + x]);
-          rovf[obase + x] = (uint16_t)e;
-          if ((e & 0xFFu) == (uint32_t)rowc_slot(s0 + rl)) own[s0 + rl] = (uint8_t)(nw + 1 - (e >> 9));
+        if (__any(x + cg > lim)) {  // entries lim.. of this row to the overflow list
+          for (int m = max(lim - x, 0); m < cg; ++m) {
+            const uint32_t c = (m < 2 || cg == 3) ? ((hz >> (8 * m)) & 0xFFu)
+                                                  : (uint32_t)csort[((hz >> 16) & 0xFFu) + m];
+            orow[x + m] = (uint16_t)(c | A);
+          }
         }
-        if (lane == 0) rovfr[s0 + rl] = (uint32_t)obase | ((uint32_t)extra << 16);
+        x += cg;
       }
     }
-    if (!fits) break;
   }
   if (__syncthreads_or(!fits)) {  // does not fit: leave the block to the fallback kernel
     if (tid == 0) {
@@ -2608,6 +2563,32 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
     }
     return;
   }
+  // -- staging -> record: word (q4, lane) holds VGPRs 4q4..4q4+3 of the lane; VGPR q
+  //    of lane 32L + x = entry x of rows 4q + 2L (low half) and 4q + 2L + 1 (high) --
+  const int nq4 = (n + 15) >> 4;
+  for (int w4 = tid; w4 < nq4 * 64; w4 += TILE_NW * WAVE) {
+    const int ln = w4 & 63, q4 = w4 >> 6, x = ln & 31, Lh = ln >> 5;
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r0 = 4 * (4 * q4 + k) + 2 * Lh;
+      uint32_t dw = 0;
+#pragma unroll
+      for (int H = 0; H < 2; ++H) {
+        const int r = r0 + H;
+        const uint32_t rc = (r < n) ? (uint32_t)rcnt[r] : 0u;
+        uint32_t e = 256u + (uint32_t)x;  // unused entry: the lane's dump slot
+        if ((uint32_t)x < (rc & 0x7Fu))
+          e = stage[r * (2 * TILE_RS) + x];
+        else if ((rc & 0x80u) && x == 31)
+          e = (256u + 31u) | (SP2_MARK << 9);
+        dw |= e << (16 * H);
+      }
+      v[k] = dw;
+    }
+    ((uint4 *)rtile)[w4] = make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  __syncthreads();
   if (tid < 64) ((uint32_t *)(rec + SP2_REC_OWN))[tid] = ((uint32_t *)own)[tid];
   if (tid == 0) *status = 0;
 }

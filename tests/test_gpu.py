@@ -773,3 +773,32 @@ def test_no_apply_solves_overlapping_blocks(sh, ctx, full_data):
         for b in range(B):
             assert np.array_equal(c[b], want[b][0]) and int(cost[b]) == want[b][1], (fl, b)
     assert ctx.error_flags() == 0
+
+
+@pytest.mark.parametrize("nw,ng,nq", [(10, 300, 100), (7, 200, 150), (10, 80, 375), (12, 100, 300)])
+def test_small_wishlists_match_oracle(sh, nw, ng, nq):
+    """Wishlists whose length is not a multiple of 4 (the tile build's generic
+    load path), odd lengths, and few gift types (types with 4+ columns in a
+    block: the column-sort spill list; rows with more than 32 hits: the
+    overflow list and, past its capacity, the fallback launch): the sparse
+    design and the LDS-tile kernel equal the oracle's round bit for bit."""
+    from santa_hip import _lib
+    from santa_hip import data as D
+    sd = D.synthetic(seed=5, nc=ng * nq, ng=ng, nq=nq, n_wish=nw, n_good=50)
+    c = sh.SantaGPU.from_data(sd, 0)
+    n = 256
+    B = min(24, c.geometry(0, n)[3])
+    rows = c.sample_blocks(0, n, B, 3, 0)
+    r = rows.cpu().numpy().reshape(B, n)
+    want_types = sd.types.copy()
+    want_col, want_cost = oracle.round_blocks(0, sd.wish, want_types, r, ng=ng)
+    for fl in (_lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_VT_TILE):
+        types = c.upload_types(sd.types)
+        col = torch.empty(B * n, dtype=torch.int32, device="cuda")
+        cost = torch.empty(B, dtype=torch.int64, device="cuda")
+        c.solve_blocks(0, rows, n, types, col=col, cost=cost, flags=fl)
+        assert np.array_equal(col.cpu().numpy().reshape(B, n), want_col), (nw, ng, fl)
+        assert np.array_equal(cost.cpu().numpy(), want_cost), (nw, ng, fl)
+        assert np.array_equal(types.cpu().numpy(), want_types), (nw, ng, fl)
+    assert c.error_flags() == 0
+    c.close()
