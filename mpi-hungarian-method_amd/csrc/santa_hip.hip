@@ -2508,8 +2508,8 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
       const int extra = (int)total - 31;
       obase = atomicAdd(ocnt, extra);
       if (obase + extra > a.cap) fits = false;  // a.cap <= SP2_OVF_CAP (tests lower it)
-      else rovfr[tid] = (uint32_t)obase | ((uint32_t)extra << 16);
     }
+    rovfr[tid] = lim == 31 ? (uint32_t)obase | ((uint32_t)(total - 31u) << 16) : 0u;  // (0: no overflow)
     rcnt[tid] = (uint8_t)(total > 32u ? 0x80u | 31u : total);
   }
   // -- pass 2: the entries (slot | a << 9, a = n_wish - rank) in wish order -------------
@@ -2624,6 +2624,7 @@ __device__ __forceinline__ uint32_t tile2_get(const u32x32 &T0, const u32x32 &T1
   return (q < 32) ? T0[q] : T1[q - 32];
 }
 
+template <bool EXACT>
 __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const unsigned char *rec_all) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
@@ -2639,10 +2640,11 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
   int64_t *u_l = (int64_t *)(smem + L.u);
   uint8_t *rem = smem + L.rem;
   uint64_t *rowc = (uint64_t *)(smem + L.rowc);
-  const int x31 = lane & 31, Lh = lane >> 5;
+  const int x31 = lane & 31;
 
   // -- the tile into VGPRs (16 coalesced 16-byte loads per lane), the rest to LDS
   u32x32 T0, T1;
+  uint32_t ovb = 0;  // bit k: row 4 * lane + k has more than 32 hits (overflow list)
   {
     const uint4 *src = (const uint4 *)(rec + SP2_REC_TILE);
     const int nq4 = (n + 15) >> 4;  // 16-byte words holding the block's rows
@@ -2657,7 +2659,11 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
     for (int x = lane; x < SP2_OVF_CAP / 2; x += WAVE) ((uint32_t *)ovf)[x] = ro[x];
     const uint32_t *rr = (const uint32_t *)(rec + SP2_REC_OVFR);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) ovfr[4 * lane + k] = rr[4 * lane + k];
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t g = rr[4 * lane + k];
+      ovfr[4 * lane + k] = g;
+      ovb |= (4 * lane + k < n && (g >> 16) != 0u) ? 1u << k : 0u;
+    }
     ((uint32_t *)own)[lane] = ((const uint32_t *)(rec + SP2_REC_OWN))[lane];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -2686,7 +2692,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
   // the final duals and every Dijkstra's minVal bound all intermediate values;
   // a block outside the range (or every block under SH_FLAG_TEST_RANGE) is
   // left untouched and re-solved by the fallback launch.
-  const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
+  constexpr bool exact = EXACT;  // (the two-pass argmin of the tests: its own instantiation)
   const uint64_t BIAS = SP2_BIAS;
   int64_t sb[4], W[4];  // spc + BIAS; -v   (columns 4*lane + k), scaled
   i32x4 path, r4c;
@@ -2743,17 +2749,23 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         const uint64_t uraw = (uint64_t)u_l[i];
         const int mover_v = rem[nrem - 1];  // the column at the last position
         const uint32_t e = (tw >> ((i & 1) << 4)) & 0xFFFFu;
-        const bool mine = Lh == ((i >> 1) & 1);
+        // the row's half of the wave (lanes 32L.., L = (i >> 1) & 1) as an SGPR mask
+        const uint64_t hmask = ((i >> 1) & 1) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+        const bool mine = __builtin_amdgcn_inverse_ballot_w64(hmask);
         const uint32_t ea = e >> 9;
-        // previous step's book-keeping (no LDS dependence)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) LM[k] &= ~__builtin_amdgcn_ballot_w64(lo[k] == kglo);
+        // previous step's book-keeping (no LDS dependence): the mover's position
+        // key first, in place, then the winner leaves the live masks (the moved
+        // column's new bits never equal the winner's: they differ in the row or
+        // column field, or the mover is the winner and its bits are unchanged)
 #pragma unroll
         for (int k = 0; k < 4; ++k) lo[k] ^= (4 * lane + k == kmover) ? kX : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) LM[k] &= ~__builtin_amdgcn_ballot_w64(lo[k] == kglo);
         // expand the row: hit columns get -a << 32, the rest hold E
         const int sslot = mine ? (int)(e & 0x1FFu) : 256 + x31;
         rowc[sslot] = (uint64_t)(uint32_t)(-(int)ea) << (32 + SP2_SH);
-        const bool ovr = __builtin_amdgcn_ballot_w64(mine && ea == SP2_MARK) != 0;
+        // (rows with more than 32 hits: a bit per row, read from the row's owner lane)
+        const bool ovr = (__builtin_amdgcn_readlane((int)ovb, i >> 2) >> (i & 3)) & 1;
         if (__builtin_expect(ovr, 0)) {
           const uint32_t rg = ovfr[i];  // more than 32 hits: the rest from the overflow area
           const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
@@ -3731,8 +3743,12 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
     else
       hipLaunchKernelGGL(santa_tile_kernel<false>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(santa_sp2_kernel, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
-                       (const unsigned char *)ctx->d_rec);
+    if (a.flags & SH_FLAG_EXACT_ARGMIN)
+      hipLaunchKernelGGL(santa_sp2_kernel<true>, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
+                         (const unsigned char *)ctx->d_rec);
+    else
+      hipLaunchKernelGGL(santa_sp2_kernel<false>, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
+                         (const unsigned char *)ctx->d_rec);
   } else if (vec)
     hipLaunchKernelGGL(santa_sp_kernel<true>, dim3(B), dim3(WAVE), lds, s, a);
   else
@@ -3829,7 +3845,7 @@ int resident_blocks(sh_ctx *ctx, int design, int mode, int n) {
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
     case SH_DESIGN_SW_TILE: return occ_blocks(ctx, santa_sw_kernel, WAVE, sw_lds_layout(ctx->ng).total);
     case SH_DESIGN_VT_TILE: return occ_blocks(ctx, santa_vt_kernel<0>, VT_WG, vt_lds_layout(ctx->ng).total);
-    case SH_DESIGN_SPARSE2: return occ_blocks(ctx, santa_sp2_kernel, WAVE, sp2_lds_layout().total);
+    case SH_DESIGN_SPARSE2: return occ_blocks(ctx, santa_sp2_kernel<false>, WAVE, sp2_lds_layout().total);
     default:
       return occ_blocks(ctx, santa_sp_kernel<true>, WAVE, sp_lds_layout(ctx->ng, sp_capacity(ctx)).total);
   }
