@@ -2064,6 +2064,9 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
     lo_free[k] = ((uint32_t)(1023 - pos) << 10) | (uint32_t)j;
     lo_asg[k] = (1u << 20) | ((uint32_t)pos << 10);
   }
+  uint64_t LM0[4];     // the columns < n (every Dijkstra starts with them live)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) LM0[k] = __builtin_amdgcn_ballot_w64(4 * lane + k < n);
   uint32_t rem0 = 0;  // rem[p] = n - 1 - p for this lane's 4 positions
 #pragma unroll
   for (int k = 0; k < 4; ++k) rem0 |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
@@ -2091,7 +2094,7 @@ __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
       int sink;
       uint32_t kglo = ~0u;        // deferred: key bits of the previous winner
       uint32_t kX = 0;            // deferred: position-key flip of the moved column
-      int kmover = -1;            //           ... and that column
+      int kmover = -1;            //           ... and that column (a VGPR: the loaded byte as is)
       for (;;) {
         ++steps;
         // row i: hit range (registers), dual u[i] (LDS broadcast)
@@ -2612,7 +2615,7 @@ __host__ __device__ __forceinline__ Sp2Lds sp2_lds_layout() {
   L.own = o;    o += 256;                      // code(i, i): row i's own (old) gift
   L.ovfr = o;   o += 256 * 4;                  // overflow range per row
   L.ovf = o;    o += (size_t)SP2_OVF_CAP * 2;  // overflow entries
-  L.u = o;      o += 256 * 8;                  // row duals
+  L.u = o;      o += (256 + 64) * 8;           // row duals (+ a dump slot per lane)
   L.rem = o;    o += 256;                      // scipy's `remaining`: column at position p
   L.rowc = o;   o += (256 + 32) * 8;           // current row: C[i][j] per column + dump slots
   L.total = o;
@@ -2705,6 +2708,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
     path[k] = -1;
     r4c[k] = -1;
   }
+  uint64_t LM0[4];     // the columns < n (every Dijkstra starts with them live)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) LM0[k] = __builtin_amdgcn_ballot_w64(4 * lane + k < n);
   uint32_t rem0 = 0;  // rem[p] = n - 1 - p for this lane's 4 positions
 #pragma unroll
   for (int k = 0; k < 4; ++k) rem0 |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
@@ -2728,9 +2734,13 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         const int j = 4 * ln + k;
         const int pos = n - 1 - j;
         sb[k] = smax;
-        lo[k] = (r4c[k] < 0) ? (((uint32_t)(255 - pos) << 8) | (uint32_t)j)
-                             : ((1u << 16) | ((uint32_t)pos << 8) | (uint32_t)r4c[k]);
-        LM[k] = __builtin_amdgcn_ballot_w64(j < n);
+        // tie bits: unassigned (r4c < 0) 255 - pos | column, assigned 1 | pos | row
+        // (a bitfield select on the sign mask: no divergent branch)
+        const uint32_t um = (uint32_t)(r4c[k] >> 31);
+        const uint32_t la = ((uint32_t)(255 - pos) << 8) | (uint32_t)j;
+        const uint32_t lb = (1u << 16) | ((uint32_t)pos << 8) | (uint32_t)r4c[k];
+        lo[k] = (um & la) | (~um & lb);
+        LM[k] = LM0[k];
       }
       ((uint32_t *)rem)[lane] = rem0;
       int nrem = n;
@@ -2739,7 +2749,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
       int sink;
       uint32_t kglo = ~0u;        // deferred: key bits of the previous winner
       uint32_t kX = 0;            // deferred: position-key flip of the moved column
-      int kmover = -1;            //           ... and that column
+      int kmover = -1;            //           ... and that column (a VGPR: the loaded byte as is)
       for (;;) {
         ++steps;
         // row i: its tile entry (one indexed VGPR move), dual u[i] (LDS broadcast;
@@ -2828,11 +2838,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
         const int last = nrem - 1;
         // the winner leaves `remaining`; the column at `last` moves to pstar
         // (applied to the registers at the top of the next step)
-        const int mover = __builtin_amdgcn_readfirstlane(mover_v);
         kglo = glo;
         kX = (uint32_t)(last ^ pstar) << 8;
-        kmover = mover;
-        rem[pstar] = (uint8_t)mover;  // (every lane, same byte; a no-op when pstar == last)
+        kmover = mover_v;
+        rem[pstar] = (uint8_t)mover_v;  // (every lane, same byte; a no-op when pstar == last)
         --nrem;
         if (!assigned) {
           sink = aux;
@@ -2845,16 +2854,19 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
       // columns).  The visited rows other than cur are the rows of the removed
       // assigned columns, and a removed column's spc is frozen since its removal
       // (it never improves again), so the column owners apply both updates;
-      // the matching makes the rows distinct (plain LDS adds, no conflicts).
+      // the matching makes the rows distinct.  Branch-free: every column adds
+      // its (masked) update with one LDS atomic add -- a visited column is
+      // assigned, the others add 0, unassigned ones to the lane's dump slot.
       // (The pending removal of the sink needs no update: spc = minVal.)
       const uint64_t mvb = (uint64_t)minVal + BIAS;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const uint64_t vis = ~LM[k] & __builtin_amdgcn_ballot_w64(4 * lane + k < n);
-        const bool vk = __builtin_amdgcn_inverse_ballot_w64(vis);
-        const int64_t d = (int64_t)(mvb - (uint64_t)sb[k]);
-        W[k] = vk ? W[k] + d : W[k];
-        if (vk && r4c[k] >= 0) u_l[r4c[k]] += d;
+        const bool vk = __builtin_amdgcn_inverse_ballot_w64(~LM[k] & LM0[k]);
+        const int64_t dd = vk ? (int64_t)(mvb - (uint64_t)sb[k]) : 0;
+        W[k] += dd;
+        const int ua = r4c[k] >= 0 ? r4c[k] : 256 + lane;
+        __hip_atomic_fetch_add((unsigned long long *)(u_l + ua), (unsigned long long)dd, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       if (lane == 0) u_l[cur] += minVal;
       mvbig |= (uint64_t)(minVal + SP2_LIM) >= 2 * (uint64_t)SP2_LIM;
