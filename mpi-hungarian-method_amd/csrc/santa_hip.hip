@@ -2623,8 +2623,10 @@ __host__ __device__ __forceinline__ Sp2Lds sp2_lds_layout() {
 }
 
 // T[q] for a wave-uniform q (one indexed VGPR move)
+// (both halves read with the same index and selected: no branch in the step)
 __device__ __forceinline__ uint32_t tile2_get(const u32x32 &T0, const u32x32 &T1, int q) {
-  return (q < 32) ? T0[q] : T1[q - 32];
+  const uint32_t a = T0[q & 31], b = T1[q & 31];
+  return (q & 32) ? b : a;
 }
 
 template <bool EXACT>
