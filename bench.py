@@ -257,7 +257,7 @@ def stored_traffic(knames):
             write = sum(e["WRITE_SIZE_bytes"] for e in es)
             return {"traffic": round(fetch * k + write),
                     "traffic_raw": {"FETCH_SIZE": fetch, "WRITE_SIZE": write, "kernels": knames,
-                                    "fetch_correction": round(k, 4)},
+                                    "fetch_correction": k},
                     "traffic_source": f"{os.path.basename(path)} (kernel source {src})"}
     return {"traffic": None,
             "traffic_note": f"no committed PMC summary was taken on this kernel source ({src})"}
