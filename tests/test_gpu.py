@@ -196,10 +196,17 @@ def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
     s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
     # singles n <= 256: the default for few blocks (LDS tile) and the forced
     # throughput kernel (sparse) are both checked
-    # (SH_FLAG_TEST_RANGE: every block of the register-tile design leaves its
-    # scaled-unit solver for the fallback launch, the path of an out-of-range block)
-    for fl in ((0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1, _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_TEST_RANGE)
-               if mode == 0 and n <= 256 else (0,)):
+    # (SH_FLAG_TEST_RANGE: every block leaves its scaled-unit solver -- the
+    # register-tile design for the fallback launch, the LDS-tile kernel for its
+    # windowed-key re-solve -- the path of an out-of-range block)
+    if mode == 0 and n <= 256:
+        flag_sets = (0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1, _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_TEST_RANGE,
+                     _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_LDS_TILE | _lib.SH_FLAG_TEST_RANGE)
+    elif mode == 1 and n <= 256:
+        flag_sets = (0, _lib.SH_FLAG_TEST_RANGE)
+    else:
+        flag_sets = (0,)
+    for fl in flag_sets:
         types = ctx.upload_types(full_data.types)
         col = torch.empty(B * n, dtype=torch.int32, device="cuda")
         cost = torch.empty(B, dtype=torch.int64, device="cuda")
