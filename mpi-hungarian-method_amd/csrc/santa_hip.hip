@@ -345,6 +345,15 @@ __device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
+// 32-bit unsigned min within each 16-lane row, held by every lane of the row
+__device__ __forceinline__ uint32_t row_min_u32_dpp(uint32_t x) {
+  x = dpp_min_step<0xB1, 0xF>(x);   // quad_perm [1,0,3,2]
+  x = dpp_min_step<0x4E, 0xF>(x);   // quad_perm [2,3,0,1]
+  x = dpp_min_step<0x141, 0xF>(x);  // row_half_mirror
+  x = dpp_min_step<0x140, 0xF>(x);  // row_mirror
+  return x;
+}
+
 // 64-bit unsigned min as two fused 32-bit reductions (high word, then the
 // low word among the lanes holding the minimal high word).
 // UNIQ: when one lane holds the minimal high word, read the low word from
@@ -493,10 +502,10 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
       if constexpr (NW == 1) {
         g = wave_min_u64_fast<true>(best);
       } else {
-        // wave DPP min of the high words; the lanes holding it (usually one)
-        // fold their full keys into the step word
+        // DPP min of the high words within each 16-lane row; the lanes holding
+        // it (usually one per row) fold their full keys into the step word
         const uint32_t bh = (uint32_t)(best >> 32);
-        const uint32_t mh = wave_min_u32_dpp(bh);
+        const uint32_t mh = row_min_u32_dpp(bh);
         if (bh == mh && mh != ~0u)
           __hip_atomic_fetch_min(S.red + par, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __syncthreads();
@@ -637,10 +646,11 @@ __device__ bool sap_solve_mw_sc(const int n, const Loader &ld, const SolveLds &S
       sb = upd ? r : sb;
       path = upd ? i : path;
       const uint64_t best = act ? ((uint64_t)sb | lo) : ~0ull;
-      // wave DPP min of the high words; the lanes holding it (usually one)
-      // fold their full keys into the step word
       const uint32_t bh = (uint32_t)(best >> 32);
-      const uint32_t mh = wave_min_u32_dpp(bh);
+      // DPP min of the high words within each 16-lane row (every lane holds its
+      // row's minimum, no row_bcast steps or readlane); the lanes holding it
+      // (usually one per row) fold their full keys into the step word
+      const uint32_t mh = row_min_u32_dpp(bh);
       if (bh == mh && mh != ~0u)
         __hip_atomic_fetch_min(S.red + par, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __syncthreads();

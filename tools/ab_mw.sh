@@ -1,0 +1,21 @@
+#!/bin/bash
+# A/B of two library builds on the latency-bound launches of the 4-wave
+# LDS-tile kernel (dev tool): one GPU's 8-GPU shard (466 blocks) at rounds 0
+# and 10, the twins round (78 blocks), a lone singles block.
+#   tools/ab_mw.sh <lib_b.so> [reps]      (A = the in-tree libsanta_hip.so)
+cd "$(dirname "$0")/.." || exit 2
+mkdir -p gpurun_out
+B=$1; R=${2:-3}
+run() {  # label lib args...
+  local lab=$1 lib=$2; shift 2
+  SANTA_HIP_LIB=$lib timeout -k 10 120 python -u tools/probe.py --phase solve --reps 3 "$@" > gpurun_out/ab1.json || exit $?
+  python3 -c "
+import json; d = json.load(open('gpurun_out/ab1.json'))
+print(json.dumps({'lib': '$lab', 'args': '$*', 'ms': round(d['solve']['ms'], 4), 'steps_max': d['steps_max']}))"
+}
+for rep in $(seq 1 "$R"); do
+  for w in "--blocks 466" "--blocks 466 --state-round 10" "--mode 1" "--blocks 1 --flags 8"; do
+    run A "" $w
+    run B "$B" $w
+  done
+done
