@@ -77,7 +77,7 @@ extern "C" {
 #define SH_DESIGN_SPARSE 0   /* one wave per block, hit lists in LDS        */
 #define SH_DESIGN_LDS_TILE 1 /* 4 waves per block, byte tile in LDS         */
 #define SH_DESIGN_SW_TILE 2  /* one wave, register tile (A/B only)          */
-#define SH_DESIGN_VT_TILE 3  /* 4 waves, register tile (A/B; nc > 2^20)     */
+#define SH_DESIGN_VT_TILE 3  /* 4 waves, register tile (one resident wave) */
 #define SH_DESIGN_TWINS 4    /* twins n <= 256: 4 waves, code-pair tile     */
 #define SH_DESIGN_LARGE 5    /* n > 256: row rebuilt from the wishlist      */
 #define SH_DESIGN_SPARSE2 6  /* one wave per block, hit tile in VGPRs       */

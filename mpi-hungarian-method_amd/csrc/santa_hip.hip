@@ -428,9 +428,9 @@ __device__ __forceinline__ uint64_t block_min_u64_rot(uint64_t wmin, uint64_t *s
   }
 }
 
-template <int NW, int K, typename Loader, int FB = 10>
-__device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, int64_t &steps_out,
-                             int &fallbacks, const bool exact) {
+template <int NW, int K, typename Loader, int FB = 10, typename... LA>
+__device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, int64_t &steps_out,
+                             int &fallbacks, const bool exact, const LA &...la) {
   // key fields: FB bits of position and of row/column (n <= 2^FB), 1 class bit
   constexpr int LOB = 2 * FB + 1;
   constexpr uint32_t FM = (1u << FB) - 1u;
@@ -473,7 +473,7 @@ __device__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, i
       ++steps;
       const int64_t ui = S.u[i];
       int64_t c[K];
-      ld.load(i, c);
+      ld.load(i, c, la...);
       if (NW > 1 && tid == 0) S.red[par == 2 ? 0 : par + 1] = ~0ull;
       const int64_t kU = minVal - ui;
       const uint64_t kb = (uint64_t)BIAS - (uint64_t)minVal;
@@ -608,9 +608,9 @@ constexpr uint32_t SC_TIE_MASK = (1u << SC_SH) - 1u;
 constexpr uint64_t SC_BIAS = 1ull << (41 + SC_SH);
 constexpr int64_t SC_LIM = 1ll << (42 + SC_SH);
 
-template <int NW, typename Loader>
-__device__ bool sap_solve_mw_sc(const int n, const Loader &ld, const SolveLds &S, int64_t &steps_out,
-                                bool big) {
+template <int NW, typename Loader, typename... LA>
+__device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, const SolveLds &S, int64_t &steps_out,
+                                bool big, const LA &...la) {
   const int tid = threadIdx.x, j = tid;
   const bool colv = j < n;
   int64_t sb = INT64_MAX, W = 0;  // spc + SC_BIAS; -v (this thread's column)
@@ -634,7 +634,7 @@ __device__ bool sap_solve_mw_sc(const int n, const Loader &ld, const SolveLds &S
       ++steps;
       const uint64_t uraw = (uint64_t)S.u[i];
       int64_t c[1];
-      ld.load(i, c);
+      ld.load(i, c, la...);
       if (tid == 0) S.red[par == 2 ? 0 : par + 1] = ~0ull;
       const int64_t ui = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uraw >> 32)) << 32) |
                                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)uraw));
@@ -1173,7 +1173,26 @@ constexpr int VT_WG = VT_NW * WAVE;
 constexpr int VT_GROUP = 32;  // virtual rows (children) staged per group
 
 struct VtLds {
-  size_t stage, rows, ctype, head, nxt, c4r, r4c, path, red, part, total;
+  size_t stage, rows, ctype, head, nxt, c4r, r4c, path, red, part, u, total;
+};
+
+// row i's cost of this thread's column from the register tile (x 2^SH);
+// singles only (the launcher never instantiates the twins register tile).
+// The tile's vectors come in as extra load() arguments (references passed
+// down the inlined call chain, as tile2_get takes them): a loader holding
+// the tile, by reference or by value, put it in scratch.
+template <int SH>
+struct VtRegLoader {
+  int nw1;
+  int64_t E;
+  __device__ __forceinline__ void load(int i, int64_t (&c)[1], const u32x32 &ta, const u32x32 &tb) const {
+    const int d = i >> 2;
+    uint32_t w0 = ta[d & 31], w1 = tb[d & 31];
+    asm volatile("" : "+v"(w0));
+    asm volatile("" : "+v"(w1));
+    const uint32_t code = (((d < 32) ? w0 : w1) >> (8 * (i & 3))) & 0xFFu;
+    c[0] = (int64_t)((uint64_t)single_cost(code, nw1, E) << SH);
+  }
 };
 
 __host__ __device__ __forceinline__ VtLds vt_lds_layout(int ng) {
@@ -1189,11 +1208,18 @@ __host__ __device__ __forceinline__ VtLds vt_lds_layout(int ng) {
   L.path = off;  off += 256 * 2;
   L.red = off;   off += 4 * VT_NW * 8;
   L.part = off;  off += r16(VT_NW * 3 * 8);
+  L.u = off;     off += 256 * 8;
   L.total = off;
   return L;
 }
 
-template <int MODE>
+// SC: the scaled-key solver (sap_solve_mw_sc); a block outside its range, or
+// every block under SH_FLAG_EXACT_ARGMIN / SH_FLAG_TEST_RANGE, is appended to
+// the overflow list untouched and re-solved by the launch of the windowed-key
+// instantiation (SC = false, also the fallback of the register-tile sparse
+// design).  One solver per instantiation: both inlined in one kernel spill
+// the tile.
+template <int MODE, bool SC>
 __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(SantaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int b = blockIdx.x;
@@ -1215,6 +1241,7 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
   int16_t *path_l = (int16_t *)(smem + L.path);
   uint64_t *red = (uint64_t *)(smem + L.red);
   int64_t *part = (int64_t *)(smem + L.part);
+  int64_t *u_l = (int64_t *)(smem + L.u);
 
   // -- rows, range check, chains ------------------------------------------------
   int bad = 0;
@@ -1335,107 +1362,36 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
   }
 
   // -- solve ------------------------------------------------------------------------
+  // (the row fetch is one indexed VGPR move from the register tile, no LDS read)
   const int nw1 = a.n_wish + 1;
   const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
-  const int64_t INF = INT64_MAX;
   const bool live = j < n;
-  int64_t spc = INF, nv = 0;
-  int path = -1, pos = -1, r4c = -1;
-  RowDuals U;
-  U.lo = u32x4{0, 0, 0, 0};
-  U.hi = u32x4{0, 0, 0, 0};
+  const SolveLds S{u_l, c4r_l, r4c_l, path_l, red};
+  if (live) u_l[j] = 0;
   int64_t steps = 0;
   int fallbacks = 0;
-  int par = 0;
   if (a.flags & SH_FLAG_BUILD_ONLY) {
     if (live) c4r_l[j] = (int16_t)j, r4c_l[j] = (int16_t)j;
     __syncthreads();
-  } else {
-    for (int cur = 0; cur < n; ++cur) {
-      spc = INF;
-      pos = live ? (n - 1 - j) : -1;
-      r4c = live ? r4c_l[j] : -1;
-      uint32_t vis = ((cur & 63) == lane) ? (1u << (cur >> 6)) : 0u;
-      int nrem = n;
-      int64_t minVal = 0;
-      int i = cur;
-      int sink;
-      for (;;) {
-        ++steps;
-        const uint32_t code = T.get(i);
-        const int64_t c = MODE ? twin_cost(code, nw1, a.E) : single_cost(code, nw1, a.E);
-        const int64_t r = c + nv - U.read(i);
-        const bool act = pos >= 0;
-        const bool upd = act && (r < spc);
-        spc = upd ? r : spc;
-        path = upd ? i : path;
-        const uint64_t kb = (uint64_t)KEY_BIAS - (uint64_t)minVal;
-        const uint32_t lo = (r4c < 0) ? (((uint32_t)(1023 - pos) << 10) | (uint32_t)j)
-                                      : ((1u << 20) | ((uint32_t)pos << 10) | (uint32_t)r4c);
-        const uint64_t key = act ? ((key_hi_of((uint64_t)spc + kb) << KEY_LO_BITS) | lo) : ~0ull;
-        uint64_t g = block_min_u64<VT_NW>(wave_min_u64_fast(key), red + par * VT_NW, w);
-        g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
-            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
-        par ^= 1;
-        const uint64_t hi = g >> KEY_LO_BITS;
-        if (exact || hi == 0 || hi == KEY_HI_MAX) {
-          uint64_t m = act ? ((uint64_t)spc ^ SIGN64) : ~0ull;
-          m = block_min_u64<VT_NW>(wave_min_u64_dpp(m), red + 2 * VT_NW, w);
-          const int64_t ms = (int64_t)(m ^ SIGN64);
-          const uint64_t b2 = (act && spc == ms) ? (uint64_t)lo : ~0ull;
-          g = block_min_u64<VT_NW>(wave_min_u64_dpp(b2), red + 3 * VT_NW, w);
-          g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
-              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
-          minVal = ms;
-          ++fallbacks;
-        } else {
-          minVal = minVal + ((int64_t)hi - KEY_BIAS);
-        }
-        const bool assigned = (g >> 20) & 1u;
-        const int pk = (int)((g >> 10) & 1023u);
-        const int aux = (int)(g & 1023u);
-        const int pstar = assigned ? pk : 1023 - pk;
-        const int last = nrem - 1;
-        pos = (pos == pstar) ? -1 : ((pos == last) ? pstar : pos);
-        --nrem;
-        if (!assigned) {
-          sink = aux;
-          break;
-        }
-        i = aux;
-        // row i is reached with minimum minVal: u~[i] -= minVal now, += the
-        // final minimum at the end (scipy: u[i] += minVal - spc[col4row[i]]).
-        U.add_owner(i, -minVal);
-        vis |= ((i & 63) == lane) ? (1u << (i >> 6)) : 0u;
-      }
-      // dual updates: visited rows (this wave's copy), visited columns (owner)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if ((vis >> k) & 1u) {
-          const uint64_t v = (((uint64_t)U.hi[k] << 32) | U.lo[k]) + (uint64_t)minVal;
-          U.lo[k] = (uint32_t)v;
-          U.hi[k] = (uint32_t)(v >> 32);
-        }
-      }
-      if (live && pos < 0) {
-        nv = nv + (minVal - spc);
-        path_l[j] = (int16_t)path;
-      }
-      __syncthreads();
-      if (tid == 0) {  // augment along the path from the sink back to cur
-        int jj = sink;
-        for (;;) {
-          const int pi = path_l[jj];
-          r4c_l[jj] = (int16_t)pi;
-          const int t = c4r_l[pi];
-          c4r_l[pi] = (int16_t)jj;
-          jj = t;
-          if (pi == cur) break;
-        }
-      }
-      __syncthreads();
+  } else if constexpr (SC) {
+    bool redo = exact;
+    if (!exact) {
+      const VtRegLoader<SC_SH> ld{nw1, a.E};
+      redo = sap_solve_mw_sc<VT_NW>(n, ld, S, steps, (a.flags & SH_FLAG_TEST_RANGE) != 0, T.a, T.b);
     }
+    if (redo) {  // (block-uniform) left untouched for the windowed-key launch
+      if (tid == 0) {
+        const int q = atomicAdd(a.ovf_cnt, 1);
+        a.ovf_list[q] = b;
+      }
+      return;
+    }
+  } else {
+    const VtRegLoader<0> ld{nw1, a.E};
+    sap_solve_mw<VT_NW, 1>(n, ld, S, steps, fallbacks, exact, T.a, T.b);
   }
+  __syncthreads();
+
   // -- outputs (column-owner view): thread j knows row r4c[j] took column j ----------
   int64_t cost = 0, dch = 0, dgh = 0;
   if (live) {
@@ -3591,6 +3547,11 @@ int fail(int code, const std::string &msg) {
     if (e_ != hipSuccess)                                                          \
       return fail(SH_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
   } while (0)
+#define HIP_TRY_RC(expr)            \
+  do {                              \
+    const int rc_ = (expr);         \
+    if (rc_ != SH_OK) return rc_;   \
+  } while (0)
 
 int pick_k(int n) {
   if (n <= 64) return 1;
@@ -3653,6 +3614,7 @@ struct sh_ctx {
   int ovf_par = 0;
   int n_cu = 0;          // compute units (LDS-tile slot count)
   int lds_slots = 0, lds_slots_n = -1;  // cached lds_tile_slots for one n
+  int vt_slots = -1;                     // cached vt_tile_slots
 };
 
 namespace {
@@ -3834,11 +3796,11 @@ int launch_santa_sw(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s)
   return SH_OK;
 }
 
-template <int MODE>
+template <int MODE, bool SC = false>
 int launch_santa_vt(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   const VtLds L = vt_lds_layout(ctx->ng);
   if (L.total > 64 * 1024) return fail(SH_ERR_ARGS, "too many gift types for the LDS chain heads");
-  hipLaunchKernelGGL((santa_vt_kernel<MODE>), dim3(B), dim3(VT_WG), L.total, s, a);
+  hipLaunchKernelGGL((santa_vt_kernel<MODE, SC>), dim3(B), dim3(VT_WG), L.total, s, a);
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
@@ -3868,6 +3830,47 @@ int launch_santa_big(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s
   return launch_big_cfg<MODE, 16, 4, 12>(ctx, a, B, s);
 }
 
+// The overflow lists of the designs with a fallback launch (block ids, two
+// counters that alternate between calls).
+int ensure_ovf(sh_ctx *ctx, int B, hipStream_t s) {
+  if (ctx->ovf_cap < B) {
+    if (ctx->d_ovf) HIP_TRY(hipFree(ctx->d_ovf));
+    ctx->d_ovf = nullptr;
+    ctx->ovf_cap = 0;
+    const int capB = std::max(B, 4096);
+    HIP_TRY(hipMalloc(&ctx->d_ovf, (2 + 2 * (size_t)capB) * sizeof(int32_t)));
+    HIP_TRY(hipMemsetAsync(ctx->d_ovf, 0, 2 * sizeof(int32_t), s));
+    ctx->ovf_cap = capB;
+    ctx->ovf_par = 0;
+  }
+  return SH_OK;
+}
+
+// Register-tile 4-wave kernel in scaled units + the windowed-key launch over
+// the blocks it left (out of range; every block under the exact-argmin and
+// range test flags).  Counters alternate as in launch_santa_sp.
+int launch_santa_vt_sc(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
+  HIP_TRY_RC(ensure_ovf(ctx, B, s));
+  const int p = ctx->ovf_par;
+  a.ovf_cnt = ctx->d_ovf + p;
+  a.ovf_list = ctx->d_ovf + 2 + (size_t)p * ctx->ovf_cap;
+  a.blist = nullptr;
+  int rc = launch_santa_vt<0, true>(ctx, a, B, s);
+  if (rc == SH_OK) {
+    SantaArgs f = a;
+    f.blist = a.ovf_list;
+    f.bcount = a.ovf_cnt;
+    f.ovf_reset = ctx->d_ovf + (p ^ 1);
+    rc = launch_santa_vt<0, false>(ctx, f, B, s);
+  }
+  if (rc) {
+    (void)hipMemsetAsync(ctx->d_ovf + p, 0, sizeof(int32_t), s);
+    return rc;
+  }
+  ctx->ovf_par = p ^ 1;
+  return SH_OK;
+}
+
 // Sparse-tile kernel + the fallback launch for blocks whose hit lists did not
 // fit.  The two overflow counters alternate between calls: the fallback
 // launch of call k resets the counter that call k+1 appends to.
@@ -3883,16 +3886,7 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
     HIP_TRY(hipMalloc(&ctx->d_rec, (size_t)capB * SP2_REC));
     ctx->rec_cap = capB;
   }
-  if (ctx->ovf_cap < B) {
-    if (ctx->d_ovf) HIP_TRY(hipFree(ctx->d_ovf));
-    ctx->d_ovf = nullptr;
-    ctx->ovf_cap = 0;
-    const int capB = std::max(B, 4096);
-    HIP_TRY(hipMalloc(&ctx->d_ovf, (2 + 2 * (size_t)capB) * sizeof(int32_t)));
-    HIP_TRY(hipMemsetAsync(ctx->d_ovf, 0, 2 * sizeof(int32_t), s));
-    ctx->ovf_cap = capB;
-    ctx->ovf_par = 0;
-  }
+  HIP_TRY_RC(ensure_ovf(ctx, B, s));
   const int p = ctx->ovf_par;
   a.cap = cap;
   a.ovf_cnt = ctx->d_ovf + p;
@@ -3954,6 +3948,17 @@ int lds_tile_slots(sh_ctx *ctx, int n) {
   return ctx->lds_slots;
 }
 
+// Register-tile 4-wave blocks (singles) the device holds at once.
+int vt_tile_slots(sh_ctx *ctx) {
+  if (ctx->vt_slots >= 0) return ctx->vt_slots;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, santa_vt_kernel<0, true>, VT_WG,
+                                                   vt_lds_layout(ctx->ng).total) != hipSuccess)
+    per_cu = 0;
+  ctx->vt_slots = per_cu * ctx->n_cu;
+  return ctx->vt_slots;
+}
+
 int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   // triplets (a few blocks per round: 1667 units) rebuild each row from the wishlists
   if (n > 256 || mode == SH_MODE_TRIPLETS) return SH_DESIGN_LARGE;
@@ -3974,6 +3979,11 @@ int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   // 4-wave tile kernel has lower (MI355X, one GPU's shard of a round at 8
   // GPUs, 466 blocks: 2.25 vs 2.41 ms at round 0, 0.81 vs 0.95 ms at round 10)
   if (B <= lds_tile_slots(ctx, n)) return SH_DESIGN_LDS_TILE;
+  // up to one resident wave of register-tile 4-wave blocks (4 per CU): the
+  // latency-bound shard of a round at 4 GPUs (933 blocks: 1.68 vs 2.13 ms at
+  // round 0, 0.67 vs 0.89 ms at round 10 for the sparse kernel; beyond it the
+  // sparse kernel's 4 blocks per SIMD win: 1865 blocks 2.45 vs 2.76 ms)
+  if (sparse == SH_DESIGN_SPARSE2 && B <= vt_tile_slots(ctx)) return SH_DESIGN_VT_TILE;
   return sparse;
 }
 
@@ -4009,7 +4019,7 @@ int resident_blocks(sh_ctx *ctx, int design, int mode, int n) {
       return occ_blocks(ctx, santa_block_kernel<1, 1>, SANTA_WG, santa_lds_layout(n, 1, ctx->ng).total);
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
     case SH_DESIGN_SW_TILE: return occ_blocks(ctx, santa_sw_kernel, WAVE, sw_lds_layout(ctx->ng).total);
-    case SH_DESIGN_VT_TILE: return occ_blocks(ctx, santa_vt_kernel<0>, VT_WG, vt_lds_layout(ctx->ng).total);
+    case SH_DESIGN_VT_TILE: return vt_tile_slots(ctx);
     case SH_DESIGN_SPARSE2: return occ_blocks(ctx, santa_sp2_kernel<false>, WAVE, sp2_lds_layout().total);
     default:
       return occ_blocks(ctx, santa_sp_kernel<true>, WAVE, sp_lds_layout(ctx->ng, sp_capacity(ctx)).total);
@@ -4046,7 +4056,7 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
     case SH_DESIGN_TWINS: return launch_santa<1, 1>(ctx, a, B, s);
     case SH_DESIGN_LDS_TILE: return launch_santa<1, 0>(ctx, a, B, s);
     case SH_DESIGN_SW_TILE: return launch_santa_sw(ctx, a, B, s);
-    case SH_DESIGN_VT_TILE: return launch_santa_vt<0>(ctx, a, B, s);
+    case SH_DESIGN_VT_TILE: return launch_santa_vt_sc(ctx, a, B, s);
     case SH_DESIGN_SPARSE2: return launch_santa_sp(ctx, a, B, s, true);
     default: return launch_santa_sp(ctx, a, B, s, false);
   }

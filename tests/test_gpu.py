@@ -201,7 +201,8 @@ def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
     # windowed-key re-solve -- the path of an out-of-range block)
     if mode == 0 and n <= 256:
         flag_sets = (0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1, _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_TEST_RANGE,
-                     _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_LDS_TILE | _lib.SH_FLAG_TEST_RANGE)
+                     _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_LDS_TILE | _lib.SH_FLAG_TEST_RANGE,
+                     _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_VT_TILE | _lib.SH_FLAG_TEST_RANGE)
     elif mode == 1 and n <= 256:
         flag_sets = (0, _lib.SH_FLAG_TEST_RANGE)
     else:
@@ -506,17 +507,43 @@ def test_kernel_designs_agree(sh, ctx, full_data):
                 assert np.array_equal(x, y), (B, nn)
 
 
+def test_shard_designs_agree(sh, ctx, full_data):
+    """One GPU's shard of a round at 4 and 8 GPUs (933 / 466 blocks, the
+    register-tile and LDS-tile 4-wave kernels by default) equals the
+    register-tile sparse kernel's result, also with every block sent through
+    the windowed-key re-solve (SH_FLAG_TEST_RANGE) and the exact argmin."""
+    from santa_hip import _lib
+    for B in (933, 466):
+        rows = ctx.sample_blocks(0, 256, B, 2017, 0)
+        outs = []
+        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_TEST_RANGE, _lib.SH_FLAG_EXACT_ARGMIN):
+            types = ctx.upload_types(full_data.types)
+            col = torch.empty(B * 256, dtype=torch.int32, device="cuda")
+            cost = torch.empty(B, dtype=torch.int64, device="cuda")
+            delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+            steps = torch.empty(B, dtype=torch.int64, device="cuda")
+            ctx.solve_blocks(0, rows, 256, types, col=col, cost=cost, delta=delta, steps=steps, flags=fl)
+            outs.append([x.cpu().numpy() for x in (col, cost, delta, steps, types)])
+        for other in outs[1:]:
+            for x, y in zip(outs[0], other):
+                assert np.array_equal(x, y), B
+    assert ctx.error_flags() == 0
+
+
 def test_design_dispatch(sh, ctx):
     """Singles n=256: the sparse kernel for a full round (3730 blocks), the
     4-wave LDS tile when the launch fits in one resident wave of LDS-tile
-    blocks (one GPU's shard at 8 GPUs: 466), the sparse kernel again when
-    forced; twins and large blocks have one design each."""
+    blocks (one GPU's shard at 8 GPUs: 466), the 4-wave register tile when it
+    fits in one resident wave of those (the shard at 4 GPUs: 933), the sparse
+    kernel again when forced; twins and large blocks have one design each."""
     from santa_hip import _lib
     assert ctx.solve_design(0, 256, 3730) == 6
     assert ctx.solve_design(0, 256, 466) == 1
     assert ctx.solve_design(0, 256, 466, _lib.SH_FLAG_SP_TILE) == 6
     assert ctx.solve_design(0, 256, 3730, _lib.SH_FLAG_SP1) == 0
-    assert ctx.solve_design(0, 256, 933) == 6
+    assert ctx.solve_design(0, 256, 933) == 3
+    assert ctx.resident_blocks(0, 256, 933) >= 933
+    assert ctx.solve_design(0, 256, 1865) == 6
     # the register-tile design holds a whole round at once (4 waves per SIMD)
     assert ctx.resident_blocks(0, 256, 3730) >= 3730
     assert ctx.solve_design(1, 256, 78) == 4
