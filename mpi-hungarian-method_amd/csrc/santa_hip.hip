@@ -929,6 +929,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
       }
     };
     if ((nw & 3) == 0) {
+      // (U = 16 loads in flight, fewer round trips to HBM, measured 3 % slower
+      // over the whole launch, the lone block included: profiles/r02b_block_build_ab.jsonl)
       constexpr int U = 4;
       const int cpr = nw >> 2;  // 8-byte chunks per row
       const int total = vrows * cpr;
@@ -978,9 +980,16 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   if (MODE) {  // code pairs -> cost-table indices (see twin_lut_index)
     for (int q = tid; q < TWIN_LUT; q += SANTA_WG) lut[q] = twin_lut_cost((uint32_t)q, a.E);
     __syncthreads();
-    uint16_t *t16 = (uint16_t *)tile8;
-    const int cnt = n * RS;
-    for (int q = tid; q < cnt; q += SANTA_WG) t16[q] = (uint16_t)twin_lut_index(t16[q], nw1);
+    // (8 entries per 16-byte LDS access; n * RS is a multiple of 16)
+    uint4 *t4 = (uint4 *)tile8;
+    const int cnt4 = n * RS / 8;
+    auto rc2 = [&](uint32_t w) -> uint32_t {
+      return twin_lut_index(w & 0xFFFFu, nw1) | (twin_lut_index(w >> 16, nw1) << 16);
+    };
+    for (int q = tid; q < cnt4; q += SANTA_WG) {
+      const uint4 v = t4[q];
+      t4[q] = make_uint4(rc2(v.x), rc2(v.y), rc2(v.z), rc2(v.w));
+    }
   }
   __syncthreads();
   // -- solve ------------------------------------------------------------------
@@ -1221,6 +1230,7 @@ __host__ __device__ __forceinline__ VtLds vt_lds_layout(int ng) {
 // the tile.
 template <int MODE, bool SC>
 __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(SantaArgs a) {
+  static_assert(MODE == 0, "singles only: VtRegLoader decodes uint8 rank codes");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
