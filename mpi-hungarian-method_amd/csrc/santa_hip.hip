@@ -599,8 +599,7 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
 // hundred happiness units, 2^40 units): the row duals only grow and the
 // column duals only fall, so each Dijkstra's minVal and the final duals
 // bound every intermediate value; sb > 0 holds because a path length is
-// never below min C - v >= min C >= -2 * 127 * 2^32 units (twins at the
-// largest n_wish sh_ctx_create accepts, 2^40 units) > -SC_BIAS / 2^SC_SH.
+// never below min C - v >= -400 happiness units (-2^39.6 units) > -SC_BIAS.
 // Returns true (block-wide) when a bound was crossed: the caller re-solves
 // with sap_solve_mw.  The loader returns costs scaled by 2^SC_SH.
 // ---------------------------------------------------------------------------
