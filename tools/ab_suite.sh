@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 B=$1; R=${2:-2}
 run() {  # label lib args...
   local lab=$1 lib=$2; shift 2
-  SANTA_HIP_LIB=$lib timeout -k 10 120 python -u tools/probe.py --phase solve --reps 3 "$@" > gpurun_out/ab1.json || exit $?
+  SANTA_HIP_LIB=${lib:-$SANTA_HIP_LIB} timeout -k 10 120 python -u tools/probe.py --phase solve --reps 3 "$@" > gpurun_out/ab1.json || exit $?
   python3 -c "
 import json; d = json.load(open('gpurun_out/ab1.json'))
 print(json.dumps({'lib': '$lab', 'args': '$*', 'ms': round(d['solve']['ms'], 4), 'steps_max': d['steps_max'],
