@@ -3100,30 +3100,22 @@ struct WishRowLoader {
   int64_t E;
   static constexpr int M = MODE + 1;                     // children per unit
   static constexpr int BPC = MODE == 0 ? 1 : 2 * MODE;  // rowbuf bytes per column
+  static_assert(NW * WAVE >= 3 * 127, "one thread per wish of a unit (n_wish <= 127)");
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int nch = (nw + 3) >> 2;
-    if (tid < M * nch) {
-      const int vr = tid / nch;  // member of the unit
-      const int cc = tid - vr * nch;
-      const int16_t *src = wish + (size_t)(rows[i] + vr) * nw;
-      uint32_t g4[4];
-      if ((nw & 3) == 0) {
-        const uint2 q = *(const uint2 *)(src + 4 * cc);
-        g4[0] = q.x & 0xFFFFu; g4[1] = q.x >> 16; g4[2] = q.y & 0xFFFFu; g4[3] = q.y >> 16;
-      } else {
-#pragma unroll
-        for (int z = 0; z < 4; ++z) g4[z] = (4 * cc + z < nw) ? (uint16_t)src[4 * cc + z] : 0xFFFFu;
-      }
-#pragma unroll
-      for (int z = 0; z < 4; ++z) {
-        const int g = (int)(int16_t)g4[z];
-        if (g >= 0) {
-          const uint32_t h = thead[g];
-          const int cnt = (int)(h >> 16), e = (int)(h & 0xFFFFu);
-          const uint8_t code = (uint8_t)(4 * cc + z + 1);
-          for (int x = e - cnt; x < e; ++x) rowbuf[BPC * csort[x] + vr] = code;
-        }
+    // one thread per wish of the unit's children (M * nw <= 381 < NW * 64):
+    // a 2-byte load of the row (100 lanes read the 200 contiguous bytes), one
+    // type-table read, the scatter of the code to the type's columns -- one
+    // short dependent chain per thread instead of four
+    if (tid < M * nw) {
+      const int vr = tid / nw;  // member of the unit
+      const int r = tid - vr * nw;
+      const int g = wish[(size_t)(rows[i] + vr) * nw + r];
+      if (g >= 0) {
+        const uint32_t h = thead[g];
+        const int cnt = (int)(h >> 16), e = (int)(h & 0xFFFFu);
+        const uint8_t code = (uint8_t)(r + 1);
+        for (int x = e - cnt; x < e; ++x) rowbuf[BPC * csort[x] + vr] = code;
       }
     }
     __syncthreads();
@@ -3833,9 +3825,15 @@ int launch_big_cfg(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) 
 template <int MODE>
 int launch_santa_big(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   const int n = a.n;
+  // a full round (at least one block per CU: 477 blocks at n = 2000) runs
+  // 8 waves per block -- half the waves per SIMD competing for issue between
+  // each block's barriers: n = 2000 round 0 113 -> 78 ms, round 5 47 -> 30 ms;
+  // a few blocks (twins at 3000 pairs: 6 per round) keep 16 (a lone block
+  // 52 vs 55 ms; profiles/r02c_big_rowbuild_ab.jsonl)
+  const bool many = B >= ctx->n_cu;
   if (n <= 512) return launch_big_cfg<MODE, 8, 1, 10>(ctx, a, B, s);
-  if (n <= 1024) return launch_big_cfg<MODE, 16, 1, 10>(ctx, a, B, s);
-  if (n <= 2048) return launch_big_cfg<MODE, 16, 2, 12>(ctx, a, B, s);
+  if (n <= 1024) return many ? launch_big_cfg<MODE, 8, 2, 10>(ctx, a, B, s) : launch_big_cfg<MODE, 16, 1, 10>(ctx, a, B, s);
+  if (n <= 2048) return many ? launch_big_cfg<MODE, 8, 4, 12>(ctx, a, B, s) : launch_big_cfg<MODE, 16, 2, 12>(ctx, a, B, s);
   if (n <= 3072) return launch_big_cfg<MODE, 16, 3, 12>(ctx, a, B, s);
   return launch_big_cfg<MODE, 16, 4, 12>(ctx, a, B, s);
 }

@@ -288,6 +288,38 @@ def test_full_round_reference_block_sizes(sh, ctx, full_data, mode, n):
     assert np.array_equal(cost.cpu().numpy()[pick], ocost)
 
 
+@pytest.mark.parametrize("n", [700, 1100, 2000])
+def test_large_block_wave_configs_agree(sh, ctx, full_data, n):
+    """Large blocks run 8 waves per block when a launch has at least one block
+    per CU and 16 otherwise: 260 blocks in one launch equal the same blocks in
+    launches of 65 (col, cost, steps, deltas, the new types), and two of them
+    equal the oracle."""
+    B = 260
+    rows = ctx.sample_blocks(0, n, B, 11, 3)
+    outs = []
+    for chunk in (B, 65):
+        types = ctx.upload_types(full_data.types)
+        col = torch.empty(B * n, dtype=torch.int32, device="cuda")
+        cost = torch.empty(B, dtype=torch.int64, device="cuda")
+        steps = torch.empty(B, dtype=torch.int64, device="cuda")
+        delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+        for b0 in range(0, B, chunk):
+            sl = slice(b0 * n, (b0 + chunk) * n)
+            d = torch.zeros(2, dtype=torch.int64, device="cuda")
+            ctx.solve_blocks(0, rows[sl], n, types, col=col[sl], cost=cost[b0:b0 + chunk],
+                             steps=steps[b0:b0 + chunk], delta=d)
+            delta += d
+        outs.append([x.cpu().numpy() for x in (col, cost, steps, delta, types)])
+    for x, y in zip(*outs):
+        assert np.array_equal(x, y), n
+    assert ctx.error_flags() == 0
+    r = rows.cpu().numpy().reshape(B, n)
+    t_host = full_data.types.copy()
+    ocol, ocost = oracle.round_blocks(0, full_data.wish, t_host, r[[5, 201]], ng=full_data.ng)
+    assert np.array_equal(outs[0][0].reshape(B, n)[[5, 201]], ocol)
+    assert np.array_equal(outs[0][1][[5, 201]], ocost)
+
+
 # --------------------------------------------------------------------------- score
 def test_score_matches_golden(sh, ctx, full_data):
     g = golden_json("santa_score.json")
