@@ -3100,7 +3100,7 @@ struct WishRowLoader {
   int64_t E;
   static constexpr int M = MODE + 1;                     // children per unit
   static constexpr int BPC = MODE == 0 ? 1 : 2 * MODE;  // rowbuf bytes per column
-  static_assert(NW * WAVE >= 3 * 127, "one thread per wish of a unit (n_wish <= 127)");
+  static_assert(NW * WAVE >= (MODE + 1) * 127, "one thread per wish of a unit (n_wish <= 127)");
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     // one thread per wish of the unit's children (M * nw <= 381 < NW * 64):
@@ -3825,14 +3825,24 @@ int launch_big_cfg(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) 
 template <int MODE>
 int launch_santa_big(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   const int n = a.n;
-  // a full round (at least one block per CU: 477 blocks at n = 2000) runs
-  // 8 waves per block -- half the waves per SIMD competing for issue between
-  // each block's barriers: n = 2000 round 0 113 -> 78 ms, round 5 47 -> 30 ms;
-  // a few blocks (twins at 3000 pairs: 6 per round) keep 16 (a lone block
-  // 52 vs 55 ms; profiles/r02c_big_rowbuild_ab.jsonl)
+  // A full round (at least one block per CU: 477 blocks at n = 2000) runs
+  // four columns per thread, so ceil(n / 256) waves per block -- fewer waves
+  // per SIMD competing for issue between each block's barriers than 16: n =
+  // 2000 round 0 113 -> 78 ms (8 waves; 4 waves x 8 columns: 93 ms), n = 1024
+  // 101 -> 30 ms and n = 600 76 -> 21 ms (4 waves); the row rebuild takes one
+  // thread per wish of a unit, (MODE + 1) * n_wish <= NW * 64.  A few blocks
+  // (twins at 3000 pairs: 6 per round, triplets) keep the wider blocks (a
+  // lone n = 2000 block: 52 ms at 16 waves, 55 at 8).
+  // (profiles/r02c_big_rowbuild_ab.jsonl, profiles/r02c_big_nw_ab.jsonl)
   const bool many = B >= ctx->n_cu;
+  if constexpr (MODE == 0) {
+    if (many && n <= 512) return launch_big_cfg<MODE, 2, 4, 10>(ctx, a, B, s);
+  }
+  if constexpr (MODE <= 1) {
+    if (many && n > 512 && n <= 1024) return launch_big_cfg<MODE, 4, 4, 10>(ctx, a, B, s);
+  }
   if (n <= 512) return launch_big_cfg<MODE, 8, 1, 10>(ctx, a, B, s);
-  if (n <= 1024) return many ? launch_big_cfg<MODE, 8, 2, 10>(ctx, a, B, s) : launch_big_cfg<MODE, 16, 1, 10>(ctx, a, B, s);
+  if (n <= 1024) return launch_big_cfg<MODE, 16, 1, 10>(ctx, a, B, s);
   if (n <= 2048) return many ? launch_big_cfg<MODE, 8, 4, 12>(ctx, a, B, s) : launch_big_cfg<MODE, 16, 2, 12>(ctx, a, B, s);
   if (n <= 3072) return launch_big_cfg<MODE, 16, 3, 12>(ctx, a, B, s);
   return launch_big_cfg<MODE, 16, 4, 12>(ctx, a, B, s);

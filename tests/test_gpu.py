@@ -288,7 +288,7 @@ def test_full_round_reference_block_sizes(sh, ctx, full_data, mode, n):
     assert np.array_equal(cost.cpu().numpy()[pick], ocost)
 
 
-@pytest.mark.parametrize("n", [700, 1100, 2000])
+@pytest.mark.parametrize("n", [300, 700, 1100, 2000])
 def test_large_block_wave_configs_agree(sh, ctx, full_data, n):
     """Large blocks run 8 waves per block when a launch has at least one block
     per CU and 16 otherwise: 260 blocks in one launch equal the same blocks in
