@@ -3110,33 +3110,37 @@ struct WishRowLoader {
     if (tid < M * nw) {
       const int vr = tid / nw;  // member of the unit
       const int r = tid - vr * nw;
-      const int g = wish[(size_t)(rows[i] + vr) * nw + r];
-      if (g >= 0) {
-        const uint32_t h = thead[g];
-        const int cnt = (int)(h >> 16), e = (int)(h & 0xFFFFu);
-        const uint8_t code = (uint8_t)(r + 1);
-        for (int x = e - cnt; x < e; ++x) rowbuf[BPC * csort[x] + vr] = code;
-      }
+      // (32-bit offset: nc * n_wish < 2^31 is checked at sh_ctx_create)
+      const int g = wish[(uint32_t)(rows[i] + vr) * (uint32_t)nw + (uint32_t)r];
+      const uint32_t h = thead[g];
+      const int cnt = (int)(h >> 16), e = (int)(h & 0xFFFFu);
+      const uint8_t code = (uint8_t)(r + 1);
+      // the type's first three columns read before any write (csort is padded:
+      // reads past the type are unused), the rest in a loop
+      const int b = e - cnt;
+      const int x0 = csort[b], x1 = csort[b + 1], x2 = csort[b + 2];
+      if (cnt > 0) rowbuf[BPC * x0 + vr] = code;
+      if (cnt > 1) rowbuf[BPC * x1 + vr] = code;
+      if (cnt > 2) rowbuf[BPC * x2 + vr] = code;
+      for (int x = b + 3; x < e; ++x) rowbuf[BPC * csort[x] + vr] = code;
     }
     __syncthreads();
+    // (every thread reads and clears its K slots: rowbuf is padded to
+    //  NW * 64 * K columns, so no per-column branch; columns >= n are inactive)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int j = w * (WAVE * K) + k * WAVE + lane;
-      if (j < n) {
-        if (MODE == 2) {
-          uint32_t *rb = (uint32_t *)rowbuf;
-          c[k] = triplet_cost(rb[j], nw1, E);
-          rb[j] = 0;
-        } else if (MODE == 1) {
-          uint16_t *rb = (uint16_t *)rowbuf;
-          c[k] = twin_cost(rb[j], nw1, E);
-          rb[j] = 0;
-        } else {
-          c[k] = single_cost(rowbuf[j], nw1, E);
-          rowbuf[j] = 0;
-        }
+      if (MODE == 2) {
+        uint32_t *rb = (uint32_t *)rowbuf;
+        c[k] = triplet_cost(rb[j], nw1, E);
+        rb[j] = 0;
+      } else if (MODE == 1) {
+        uint16_t *rb = (uint16_t *)rowbuf;
+        c[k] = twin_cost(rb[j], nw1, E);
+        rb[j] = 0;
       } else {
-        c[k] = 0;
+        c[k] = single_cost(rowbuf[j], nw1, E);
+        rowbuf[j] = 0;
       }
     }
   }
@@ -3156,9 +3160,9 @@ __host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int n
   L.red = o;    o += r16((size_t)4 * nw * 8);
   L.rows = o;   o += r16((size_t)n * 4);
   L.ctype = o;  o += r16((size_t)n * 2);
-  L.csort = o;  o += r16((size_t)n * 2);
+  L.csort = o;  o += r16((size_t)(n + 2) * 2);  // (+2: the row rebuild reads three entries per type)
   L.thead = o;  o += r16((size_t)ng * 4);
-  L.rowbuf = o; o += r16((size_t)n * (mode == 0 ? 1 : 2 * mode));
+  L.rowbuf = o; o += r16((size_t)(n + nw * 64) * (mode == 0 ? 1 : 2 * mode));  // (padded to NW * 64 * K columns)
   L.part = o;   o += r16((size_t)nw * 3 * 8);
   L.scan = o;   o += r16((size_t)nw * 4);
   L.total = o;
@@ -3649,6 +3653,8 @@ int sh_ctx_create(sh_ctx **out, int device, const int16_t *h_wish, int n_wish,
     return fail(SH_ERR_ARGS, "need nc, ng, nq > 0");
   if (n_wish <= 0 || n_wish > 127 || n_wish > ng)
     return fail(SH_ERR_ARGS, "n_wish must be in [1, min(127, ng)]");
+  if ((size_t)nc * (size_t)n_wish >= ((size_t)1 << 31))
+    return fail(SH_ERR_ARGS, "nc * n_wish must be below 2^31 (32-bit wishlist offsets)");
   if (n_good <= 0 || n_good > 32767 || n_good > nc)
     return fail(SH_ERR_ARGS, "n_good must be in [1, min(32767, nc)]");
   if (ng > 8192) return fail(SH_ERR_ARGS, "ng > 8192 unsupported (LDS chain heads)");
