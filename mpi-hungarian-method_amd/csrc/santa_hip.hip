@@ -3098,6 +3098,7 @@ struct WishRowLoader {
   uint8_t *rowbuf;        // LDS [n] (singles) / [2n] (twins: c1 | c2 << 8) / [4n] (triplets)
   int n, nw, nw1;
   int64_t E;
+  const int64_t *lut;     // twins: twin_lut_index -> exact cost (LDS), as the 4-wave twins kernel
   static constexpr int M = MODE + 1;                     // children per unit
   static constexpr int BPC = MODE == 0 ? 1 : 2 * MODE;  // rowbuf bytes per column
   static_assert(NW * WAVE >= (MODE + 1) * 127, "one thread per wish of a unit (n_wish <= 127)");
@@ -3136,7 +3137,7 @@ struct WishRowLoader {
         rb[j] = 0;
       } else if (MODE == 1) {
         uint16_t *rb = (uint16_t *)rowbuf;
-        c[k] = twin_cost(rb[j], nw1, E);
+        c[k] = lut[twin_lut_index(rb[j], nw1)];  // (one LDS read instead of the float32 rounding)
         rb[j] = 0;
       } else {
         c[k] = single_cost(rowbuf[j], nw1, E);
@@ -3147,7 +3148,7 @@ struct WishRowLoader {
 };
 
 struct BigLds {
-  size_t u, c4r, r4c, path, red, rows, ctype, csort, thead, rowbuf, part, scan, total;
+  size_t u, c4r, r4c, path, red, rows, ctype, csort, thead, rowbuf, part, scan, lut, total;
 };
 
 __host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int ng, int nw) {
@@ -3165,6 +3166,7 @@ __host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int n
   L.rowbuf = o; o += r16((size_t)(n + nw * 64) * (mode == 0 ? 1 : 2 * mode));  // (padded to NW * 64 * K columns)
   L.part = o;   o += r16((size_t)nw * 3 * 8);
   L.scan = o;   o += r16((size_t)nw * 4);
+  L.lut = o;    o += mode == 1 ? (size_t)TWIN_LUT * 8 : 0;
   L.total = o;
   return L;
 }
@@ -3207,7 +3209,10 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
     return;
   }
   for (int t = tid; t < a.ng; t += WG) thead[t] = 0u;
-  for (int q = tid; q < n * WishRowLoader<MODE, NW, K>::BPC; q += WG) rowbuf[q] = 0;
+  for (int q = tid; q < (n + WG) * WishRowLoader<MODE, NW, K>::BPC; q += WG) rowbuf[q] = 0;  // (with the padding)
+  int64_t *lut = (int64_t *)(smem + L.lut);
+  if constexpr (MODE == 1)
+    for (int q = tid; q < TWIN_LUT; q += WG) lut[q] = twin_lut_cost((uint32_t)q, a.E);
   for (int i = tid; i < n; i += WG) {
     S.u[i] = 0;
     S.c4r[i] = -1;
@@ -3256,7 +3261,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
     for (int i = tid; i < n; i += WG) S.c4r[i] = (int16_t)i;
     __syncthreads();
   } else {
-    const WishRowLoader<MODE, NW, K> ld{a.wish, rows_l, thead, csort, rowbuf, n, a.n_wish, nw1, a.E};
+    const WishRowLoader<MODE, NW, K> ld{a.wish, rows_l, thead, csort, rowbuf, n, a.n_wish, nw1, a.E, lut};
     sap_solve_mw<NW, K, WishRowLoader<MODE, NW, K>, FB>(n, ld, S, steps, fallbacks,
                                                          (a.flags & SH_FLAG_EXACT_ARGMIN) != 0);
   }
