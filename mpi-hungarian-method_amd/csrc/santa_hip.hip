@@ -3126,8 +3126,8 @@ struct WishRowLoader {
       for (int x = b + 3; x < e; ++x) rowbuf[BPC * csort[x] + vr] = code;
     }
     __syncthreads();
-    // (every thread reads and clears its K slots: rowbuf is padded to
-    //  NW * 64 * K columns, so no per-column branch; columns >= n are inactive)
+    // (every thread reads and clears its K slots: rowbuf covers NW * 64 * K
+    //  columns, so no per-column branch; columns >= n are inactive)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int j = w * (WAVE * K) + k * WAVE + lane;
@@ -3151,7 +3151,9 @@ struct BigLds {
   size_t u, c4r, r4c, path, red, rows, ctype, csort, thead, rowbuf, part, scan, lut, total;
 };
 
-__host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int ng, int nw) {
+// (the row buffer covers the NW * 64 * K columns the solver's threads own:
+//  they read and clear their K slots without a per-column branch)
+__host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int ng, int nw, int k) {
   BigLds L;
   size_t o = 0;
   L.u = o;      o += r16((size_t)n * 8);
@@ -3163,7 +3165,7 @@ __host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int n
   L.ctype = o;  o += r16((size_t)n * 2);
   L.csort = o;  o += r16((size_t)(n + 2) * 2);  // (+2: the row rebuild reads three entries per type)
   L.thead = o;  o += r16((size_t)ng * 4);
-  L.rowbuf = o; o += r16((size_t)(n + nw * 64) * (mode == 0 ? 1 : 2 * mode));  // (padded to NW * 64 * K columns)
+  L.rowbuf = o; o += r16((size_t)(nw * 64 * k) * (mode == 0 ? 1 : 2 * mode));
   L.part = o;   o += r16((size_t)nw * 3 * 8);
   L.scan = o;   o += r16((size_t)nw * 4);
   L.lut = o;    o += mode == 1 ? (size_t)TWIN_LUT * 8 : 0;
@@ -3186,7 +3188,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n = a.n;
-  const BigLds L = big_lds_layout(n, MODE, a.ng, NW);
+  const BigLds L = big_lds_layout(n, MODE, a.ng, NW, K);
   SolveLds S{(int64_t *)(smem + L.u), (int16_t *)(smem + L.c4r), (int16_t *)(smem + L.r4c),
              (int16_t *)(smem + L.path), (uint64_t *)(smem + L.red)};
   int32_t *rows_l = (int32_t *)(smem + L.rows);
@@ -3209,7 +3211,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
     return;
   }
   for (int t = tid; t < a.ng; t += WG) thead[t] = 0u;
-  for (int q = tid; q < (n + WG) * WishRowLoader<MODE, NW, K>::BPC; q += WG) rowbuf[q] = 0;  // (with the padding)
+  for (int q = tid; q < WG * K * WishRowLoader<MODE, NW, K>::BPC; q += WG) rowbuf[q] = 0;  // (the whole padded buffer)
   int64_t *lut = (int64_t *)(smem + L.lut);
   if constexpr (MODE == 1)
     for (int q = tid; q < TWIN_LUT; q += WG) lut[q] = twin_lut_cost((uint32_t)q, a.E);
@@ -3820,7 +3822,8 @@ int launch_santa_vt(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s)
 
 template <int MODE, int NW, int K, int FB>
 int launch_big_cfg(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
-  const BigLds L = big_lds_layout(a.n, MODE, ctx->ng, NW);
+  if (a.n > NW * WAVE * K) return fail(SH_ERR_ARGS, "large-block config covers fewer columns than n");
+  const BigLds L = big_lds_layout(a.n, MODE, ctx->ng, NW, K);
   if (L.total > 160 * 1024) return fail(SH_ERR_ARGS, "block too large for LDS");
   static thread_local AttrCache attr;
   if (L.total > 64 * 1024 && attr.need(ctx->device, L.total)) {
@@ -4030,7 +4033,7 @@ int occ_blocks(const sh_ctx *ctx, F f, int threads, size_t lds) {
 template <int MODE>
 int big_resident(const sh_ctx *ctx, int n) {  // mirrors launch_santa_big's configurations
 #define BR_(NW, K, FB) \
-  return occ_blocks(ctx, santa_big_kernel<MODE, NW, K, FB>, NW * WAVE, big_lds_layout(n, MODE, ctx->ng, NW).total)
+  return occ_blocks(ctx, santa_big_kernel<MODE, NW, K, FB>, NW * WAVE, big_lds_layout(n, MODE, ctx->ng, NW, K).total)
   if (n <= 512) BR_(8, 1, 10);
   if (n <= 1024) BR_(16, 1, 10);
   if (n <= 2048) BR_(16, 2, 12);
