@@ -4176,12 +4176,19 @@ int launch_lsap_i64(const S *C, uint64_t seed, int64_t mod, int n, int B, int32_
                     int64_t *cost, unsigned flags, hipStream_t s) {
   const int rc = check_lsap_args(n, B, col);
   if (rc || B == 0) return rc;
-  const int NW = n <= WAVE ? 1 : 4;
-  const size_t lds = r16((size_t)n * 8) + 3 * r16((size_t)n * 2) + r16((size_t)4 * NW * 8) + 64;
+  const size_t lds = r16((size_t)n * 8) + 3 * r16((size_t)n * 2) + r16((size_t)4 * 4 * 8) + 64;
 #define L_(NWW, KK)                                                                            \
   hipLaunchKernelGGL((lsap_i64_kernel<NWW, KK, S, HASH>), dim3(B), dim3(NWW * WAVE), lds, s, C, \
                      seed, mod, n, col, cost, (int32_t *)nullptr, flags)
-  if (NW == 1) L_(1, 1);
+  // a batch that fills the chip many times over runs one wave per instance
+  // with several columns per thread (fewer waves per block, more blocks per
+  // CU: the large-block kernel's lesson): n <= 128 from 4096 instances
+  // (65536 hash-generated: 1.45 -> 2.49 M solves/s), n = 256 from 65536
+  // (397 -> 443 k/s; at 4096 it lost 17 %); n = 512 gained nothing
+  // (profiles/r02e_lsap_sweep_ab.jsonl)
+  if (n <= WAVE) L_(1, 1);
+  else if (B >= 4096 && n <= 128) L_(1, 2);
+  else if (B >= 65536 && n <= 256) L_(1, 4);
   else if (n <= 256) L_(4, 1);
   else if (n <= 512) L_(4, 2);
   else L_(4, 4);

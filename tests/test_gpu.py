@@ -617,6 +617,24 @@ def test_exchange_over_rccl(sh, ctx, full_data):
 
 
 # --------------------------------------------------------------------------- edge sizes
+@pytest.mark.parametrize("n,B,picks", [(100, 4096, (0, 1, 4095)), (128, 8192, (7, 8191)),
+                                      (256, 65536, (0, 65535))])
+def test_lsap_large_batch_configs_vs_oracle(sh, n, B, picks):
+    """Large batches run one wave per instance with several columns per
+    thread (n <= 128 from 4096 instances, n = 256 from 65536): instances of
+    the device-generated stream equal the oracle on the host mirror of the
+    hash, permutation and cost."""
+    from santa_hip import lsap as L
+    from santa_hip.sampler import hash_matrix
+    col, cost = L.solve_hash(5, 1 << 16, n, B, device=0)
+    c = col.cpu().numpy().reshape(B, n)
+    for b in picks:
+        C = hash_matrix(5, b, n, 1 << 16).astype(np.int64)[None]
+        ocol, ocost = oracle.lsap_i64_batched(C)
+        assert np.array_equal(c[b], ocol[0]), (n, B, b)
+        assert int(cost.cpu()[b]) == int(ocost[0]), (n, B, b)
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 255])
 def test_lsap_edge_sizes_vs_oracle(sh, n):
     """Wave-boundary and degenerate sizes (one lane, partial waves, one column
