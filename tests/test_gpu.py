@@ -181,6 +181,8 @@ def test_santa_blocks_golden_reference_sizes(sh, ctx, full_data):
                                       # mpi_twins.py:244)
                                       (0, 257, 3), (0, 700, 2), (0, 1024, 2), (0, 2000, 2),
                                       (1, 300, 2), (1, 1500, 1), (1, 3000, 1),
+                                      # the largest block the boundary accepts (SH_MAX_N_SANTA)
+                                      (0, 4096, 1), (1, 4096, 1),
                                       # triplet units (extension; always the row-rebuild design)
                                       (2, 256, 6), (2, 100, 5), (2, 37, 4), (2, 555, 3)])
 def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
@@ -408,6 +410,8 @@ def test_error_paths(sh, ctx, full_data):
     assert np.array_equal(types.cpu().numpy(), full_data.types)  # skipped block wrote nothing
     with pytest.raises(ValueError):
         ctx.solve_blocks(0, torch.zeros(5000, dtype=torch.int32, device="cuda"), 5000, types)
+    with pytest.raises(ValueError):  # one past SH_MAX_N_SANTA
+        ctx.solve_blocks(0, torch.zeros(4097, dtype=torch.int32, device="cuda"), 4097, types)
     with pytest.raises(ValueError):
         ctx.sample_blocks(0, 256, 5000, 1, 0)
     with pytest.raises(ValueError):
