@@ -2802,6 +2802,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
     *(u64x2 *)(rowc + 4 * lane + 2) = E2;
   }
   __syncthreads();
+  __builtin_amdgcn_s_setprio(3);  // (lowered over the last Dijkstras, below)
   const uint64_t m1 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
 
   // -- solve (santa_sp_kernel's step; the row's hits come from the tile) -----------
@@ -2842,6 +2843,15 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
     c4r = (uint32_t)(4 * lane) * 0x01010101u + 0x03020100u;
   } else {
     for (int cur = 0; cur < n; ++cur) {
+      // Issue priority falls over the block's last Dijkstras (n-32, n-8, n-2):
+      // the four blocks sharing a SIMD share its VALU issue, and a block near
+      // its end has the least work left, so the blocks that lag behind (the
+      // long ones, which set the round's time) take the issue slots first.
+      // An approximation of longest-remaining-first: -14 % (round 0) / -12 %
+      // (round 10) per full round, profiles/r02g_setprio_ab.jsonl.
+      if (cur == n - 32) __builtin_amdgcn_s_setprio(2);
+      if (cur == n - 8) __builtin_amdgcn_s_setprio(1);
+      if (cur == n - 2) __builtin_amdgcn_s_setprio(0);
       // Dijkstra set-up: remaining = [n-1 .. 0], all columns live.  (The lane
       // id goes through an empty asm so that the per-column constants below
       // are recomputed here rather than kept live, or spilled, across the loop.)
