@@ -46,10 +46,13 @@ def parse():
     ap.add_argument("--n", type=int, default=256)
     ap.add_argument("--seed", type=int, default=2017)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="budget of the CPU port / scipy baselines (rank 0, N=1 only)")
+                    help="budget of the CPU port / scipy baselines (rank 0, before the GPU run)")
     ap.add_argument("--b1-seconds", type=float, default=6.0,
                     help="budget per rank count of the reference-semantics baseline B1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--score-check-every", type=int, default=None,
+                    help="0: rescore the whole state every round (the reference); K: the delta "
+                         "all-reduce with a full rescore every K rounds (default: 16 at N > 1, 0 at N = 1)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="test only: 'gloo' with --one-device rehearses N ranks on one GPU")
     ap.add_argument("--one-device", action="store_true",
@@ -72,8 +75,22 @@ def launch_ranks(args) -> int:
            os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # the CPU baselines run here, before any rank exists (this process touches
+    # no GPU), and reach rank 0 through a file
+    path = None
+    if not args.no_cpu_baseline and CPU_JSON_ENV not in env:
+        import tempfile
+        cb = cpu_baselines(args, cpu_info())
+        fd, path = tempfile.mkstemp(prefix="santa_bench_cpu_", suffix=".json")
+        with os.fdopen(fd, "w") as f:
+            json.dump(cb, f)
+        env[CPU_JSON_ENV] = path
     env.setdefault("OMP_NUM_THREADS", "1")
-    return subprocess.call(cmd, env=env)
+    try:
+        return subprocess.call(cmd, env=env)
+    finally:
+        if path:
+            os.unlink(path)
 
 
 # --------------------------------------------------------------------------- CPU side
@@ -113,6 +130,36 @@ def b1_baseline(mode: str, n: int, cores: int, seconds: float) -> dict:
             "score_gain_per_s": {str(x["procs"]): x["score_gain_per_s"] for x in out["runs"]},
             "rounds": {str(x["procs"]): x["rounds"] for x in out["runs"]},
             "setup_s": out["setup_s"]}
+
+
+CPU_JSON_ENV = "SANTA_BENCH_CPU_JSON"
+
+
+def cpu_baselines(args, cpu: dict) -> dict:
+    """Every CPU figure of the line, timed before this process touches the GPU
+    (rank 0, or the `--gpus N` launcher before it starts the ranks): B1 (the
+    reference's round as written, in a child process), the C port of the path
+    on the leased cores and saturated scipy.  Same workload as the GPU line."""
+    b1 = b1_baseline(args.mode, args.n, cpu["used"], args.b1_seconds) if args.mode != "triplets" else None
+    from santa_hip import data as D
+    sd = D.synthetic(args.seed)
+    mode = {"single": 0, "twins": 1, "triplets": 2}[args.mode]
+    cb = cpu_baseline(sd, mode, args.n, args.cpu_seconds, cpu["used"])
+    cb["cpu_model"] = cpu["model"]
+    cb["nproc"] = cpu["nproc"]
+    if b1 is not None and "blocks_per_s" in b1:
+        cb["b1_blocks_per_s"] = b1["blocks_per_s"]
+        cb["b1_score_gain_per_s"] = b1["score_gain_per_s"]
+        script = "mpi_single.py:119-181" if args.mode == "single" else "mpi_twins.py:121-187"
+        cb["b1_sample"] = (f"oracle/ref_semantics.py: the reference's round as written "
+                           f"({script}) with P ranks = {list(b1['blocks_per_s'])} "
+                           f"worker processes, {b1['rounds']} rounds in {args.b1_seconds}s each: "
+                           f"P blocks per round, Python n^2 cost loop, scipy, pickled "
+                           f"gather/bcast, full rescore and the 1M-row CSV per round")
+    elif b1 is not None:
+        cb["b1_error"] = b1.get("error")
+    cb["timed"] = "before the GPU run, on the host cores this rank (or the launcher) leases"
+    return cb
 
 
 def cpu_baseline(sd, mode: int, n: int, seconds: float, cores: int):
@@ -226,10 +273,10 @@ def scipy_baseline(sd, mode, n, seconds, ncores, rows, lo, count, stride, nb):
 # --------------------------------------------------------------------------- HBM traffic
 def design_kernels(kname: str):
     """The kernels one solve launch of a design runs (the register-tile sparse
-    design builds its tiles in santa_tile_kernel, then solves in santa_sp2_kernel;
+    design builds its tiles in santa_tile_kernel, then solves in santa_sp3_kernel;
     the events around the solve bracket both)."""
     k = kname.split(" ")[0].split("<")[0]
-    return ["santa_tile_kernel", k] if k == "santa_sp2_kernel" else [k]
+    return ["santa_tile_kernel", k] if k in ("santa_sp2_kernel", "santa_sp3_kernel") else [k]
 
 
 def stored_traffic(knames):
@@ -275,11 +322,17 @@ def main():
                  f"--nproc-per-node {args.gpus} or drop WORLD_SIZE")
     local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", "0"))
     cpu = cpu_info()
-    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
-    # B1 first, in a child process, while nothing here has touched the GPU
+    # the CPU baselines first, while nothing here has touched the GPU (rank 0
+    # only; the other ranks wait in the rendezvous), or the launcher's
     # (the reference has no triplet script: no B1 for the triplet extension)
-    b1 = (b1_baseline(args.mode, args.n, cpu["used"], args.b1_seconds)
-          if want_cpu and args.mode != "triplets" else None)
+    cpu_line = None
+    if rank == 0 and not args.no_cpu_baseline:
+        pre = os.environ.get(CPU_JSON_ENV)
+        if pre and os.path.exists(pre):
+            with open(pre) as f:
+                cpu_line = json.load(f)
+        else:
+            cpu_line = cpu_baselines(args, cpu)
 
     import torch
     import santa_hip
@@ -292,11 +345,14 @@ def main():
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
+        wait = datetime.timedelta(minutes=30)  # (rank 0 may time the CPU baselines first)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=dev, timeout=wait)  # RCCL over xGMI
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(args.dist_backend, timeout=wait)
     mode = {"single": _lib.SH_MODE_SINGLE, "twins": _lib.SH_MODE_TWINS,
             "triplets": _lib.SH_MODE_TRIPLETS}[args.mode]
     n = args.n
@@ -320,14 +376,15 @@ def main():
             self.timed = False
             self.ev = []
 
-        def solve_blocks(self, mode_, rows_, n_, types_):
+        def solve_blocks(self, mode_, rows_, n_, types_, delta=None):
             if not self.timed:
-                return self.ctx.solve_blocks(mode_, rows_, n_, types_)
+                return self.ctx.solve_blocks(mode_, rows_, n_, types_, delta=delta)
             k = len(self.ev)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            self.ctx.solve_blocks(mode_, rows_, n_, types_, steps=steps_dev[k] if k < max_calls else None)
+            self.ctx.solve_blocks(mode_, rows_, n_, types_, delta=delta,
+                                  steps=steps_dev[k] if k < max_calls else None)
             e1.record(stream)
             self.ev.append((e0, e1))
 
@@ -342,7 +399,8 @@ def main():
         # improving rounds, speculated and re-run after a rejection); a fixed
         # number of rounds (no patience stop) so every run times K rounds
         return run_rounds(eng, types, mode=mode, n=n, seed=args.seed, max_rounds=k, patience=1 << 30,
-                          world=w, score0=score0, pipeline=True)
+                          world=w, score0=score0, sums0=(sc0, sg0), pipeline=True,
+                          score_check_every=args.score_check_every)
 
     # warm up on the same rounds, then restart from the baseline assignment so
     # the timed rounds are rounds 0..K-1 of the optimisation (as in the
@@ -393,7 +451,8 @@ def main():
         bmax = int(st[0].argmax())
         rows0 = ctx.sample_blocks(mode, n, nb, args.seed, 0)
         one = rows0[(b0 + bmax) * n:(b0 + bmax + 1) * n].contiguous()
-        force = {0: _lib.SH_FLAG_SP_TILE, 6: _lib.SH_FLAG_SP_TILE, 1: _lib.SH_FLAG_LDS_TILE}.get(design, 0)
+        force = {0: _lib.SH_FLAG_SP_TILE, 6: _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_SP2, 7: _lib.SH_FLAG_SP_TILE,
+                 1: _lib.SH_FLAG_LDS_TILE}.get(design, 0)
         lone = []
         for _ in range(3):
             tt = ctx.upload_types(sd.types)
@@ -465,21 +524,8 @@ def main():
     }
     if world == 1:  # the PMC passes profile a full one-GPU round (tools/profile_round.sh)
         out["roofline"].update(stored_traffic(design_kernels(kname)))
-    if want_cpu:
-        cb = cpu_baseline(sd, mode, n, args.cpu_seconds, cpu["used"])
-        cb["cpu_model"] = cpu["model"]
-        cb["nproc"] = cpu["nproc"]
-        if b1 is not None and "blocks_per_s" in b1:
-            cb["b1_blocks_per_s"] = b1["blocks_per_s"]
-            cb["b1_score_gain_per_s"] = b1["score_gain_per_s"]
-            cb["b1_sample"] = (f"oracle/ref_semantics.py: the reference's round as written "
-                               f"(mpi_single.py:119-181) with P ranks = {list(b1['blocks_per_s'])} "
-                               f"worker processes, {b1['rounds']} rounds in {args.b1_seconds}s each: "
-                               f"P blocks per round, Python n^2 cost loop, scipy, pickled "
-                               f"gather/bcast, full rescore and the 1M-row CSV per round")
-        elif b1 is not None:
-            cb["b1_error"] = b1.get("error")
-        out["cpu_baseline"] = cb
+    if cpu_line is not None:
+        out["cpu_baseline"] = cpu_line
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -50,12 +50,13 @@ extern "C" {
 #define SH_FLAG_BUILD_ONLY 4u   /* sh_solve_blocks: build the cost tiles and
                                    apply the identity (phase timing only)  */
 #define SH_FLAG_LDS_TILE 8u     /* sh_solve_blocks, singles n <= 256:      */
-#define SH_FLAG_SW_TILE 16u     /* alternative kernel designs (4-wave LDS  */
-#define SH_FLAG_VT_TILE 32u     /* tile / one-wave register tile / 4-wave
-                                   register tile) kept for A/B profiling;
-                                   identical results.  Default: one-wave
-                                   sparse LDS tile (+ register-tile fallback
-                                   for blocks whose hit lists overflow)    */
+#define SH_FLAG_VT_TILE 32u     /* alternative kernel designs (4-wave LDS
+                                   tile / 4-wave register tile) kept for A/B
+                                   profiling; identical results.  Default:
+                                   see sh_solve_design                     */
+#define SH_FLAG_SW_TILE 16u     /* RETIRED (round 3): the one-wave register-
+                                   tile kernel left the library; every entry
+                                   point returns SH_ERR_ARGS for this flag */
 #define SH_FLAG_TIMING 64u      /* dev: the sparse kernel writes phase times
                                    (wall-clock ticks since its start, 3 x 21
                                    bits: built, solved, done) into d_steps */
@@ -68,6 +69,10 @@ extern "C" {
                                    treats every block as outside its
                                    scaled-unit range, so all blocks take the
                                    fallback launch (same results)          */
+#define SH_FLAG_SP2 2048u      /* force the 64-bit-key one-wave register-tile
+                                   solver (santa_sp2_kernel, round 2's
+                                   default) instead of santa_sp3_kernel (A/B;
+                                   identical results)                      */
 #define SH_FLAG_NO_APPLY 1024u  /* solve and report (col, cost, deltas,
                                    steps) but leave the gift types untouched:
                                    blocks may then overlap (batched
@@ -76,11 +81,13 @@ extern "C" {
 /* Kernel designs sh_solve_blocks can dispatch to (sh_solve_design).        */
 #define SH_DESIGN_SPARSE 0   /* one wave per block, hit lists in LDS        */
 #define SH_DESIGN_LDS_TILE 1 /* 4 waves per block, byte tile in LDS         */
-#define SH_DESIGN_SW_TILE 2  /* one wave, register tile (A/B only)          */
+#define SH_DESIGN_SW_TILE 2  /* retired (never returned)                    */
 #define SH_DESIGN_VT_TILE 3  /* 4 waves, register tile (one resident wave) */
 #define SH_DESIGN_TWINS 4    /* twins n <= 256: 4 waves, code-pair tile     */
 #define SH_DESIGN_LARGE 5    /* n > 256: row rebuilt from the wishlist      */
-#define SH_DESIGN_SPARSE2 6  /* one wave per block, hit tile in VGPRs       */
+#define SH_DESIGN_SPARSE2 6  /* one wave per block, hit tile in VGPRs,
+                                64-bit keys (SH_FLAG_SP2)                   */
+#define SH_DESIGN_SPARSE3 7  /* as 6 with 32-bit lattice keys (default)     */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024

@@ -379,13 +379,6 @@ constexpr uint64_t KEY_HI_MAX = (1ull << 43) - 1;
 constexpr int64_t KEY_BIAS = 1ll << 42;
 constexpr uint64_t SIGN64 = 0x8000000000000000ull;
 
-// clamp(spc - minVal + 2^42, 0, 2^43-1) from sb = spc + (2^42 - minVal) in
-// wrapping arithmetic; exact while |spc|, |minVal| < 2^62 (santa_hip.h bounds
-// |C| so that this holds).
-__device__ __forceinline__ uint64_t key_hi_of(uint64_t sb) {
-  return (sb <= KEY_HI_MAX) ? sb : (((int64_t)sb < 0) ? 0 : KEY_HI_MAX);
-}
-
 struct SolveLds {
   int64_t *u;       // [n]   row duals
   int16_t *c4r;     // [n]   col4row (the result)
@@ -1461,349 +1454,6 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
     if (a.delta) {
       atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)td0);
       atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)td1);
-    }
-    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Single-wave register kernel (singles, n <= 256): the production path.
-//
-// One wave64 per block, lane l owns columns l + 64k (k < 4).  Everything the
-// Dijkstra loop touches is in registers:
-//   tile  256 dwords per lane: dword r = the uint8 codes of the lane's four
-//         columns at row r, read with a wave-uniform r (s_set_gpr_idx);
-//   duals u (row r in lane r&63, slot r>>6), -v and spc/pos/path/row4col per
-//         owned column, col4row per owned row;
-// cross-lane values move with readlane, so a step has no LDS access and no
-// barrier.  The row-dual bookkeeping is the per-wave scheme of the
-// register-tile kernel above (u~[i] -= m when row i is reached, += final
-// minimum at the end), and the argmin is the same packed key, one 64-bit
-// wave-min per step.  The block cost is sum(u) + sum(v) (complementary
-// slackness holds exactly in integer arithmetic for the matched pairs), and a
-// matched entry's code is recovered from its reduced-cost identity
-// C[i][col] = u[i] + v[col].  1 wave per SIMD (~310 VGPRs), 4 blocks per CU.
-// ---------------------------------------------------------------------------
-constexpr int SW_REG_ROWS = 128;  // tile rows held in VGPRs; the rest in LDS
-
-struct SwLds {
-  size_t tile, rows, ctype, head, nxt, total;
-};
-
-__host__ __device__ __forceinline__ SwLds sw_lds_layout(int ng) {
-  SwLds L;
-  size_t off = 0;
-  L.tile = off;  off += (size_t)128 * 256;  // rows 128..255 [row][lane*4 + k]; stage for 0..127
-  L.rows = off;  off += 256 * 4;
-  L.ctype = off; off += 256 * 2;
-  L.head = off;  off += r16((size_t)ng * 4);
-  L.nxt = off;   off += 256 * 2;
-  L.total = off;
-  return L;
-}
-
-// dword r (< 128) of the register tile = codes of columns (l, l+64, l+128,
-// l+192) at row r; r wave-uniform.  By-value vectors (not a struct member
-// access through `this`) so that SROA keeps them in VGPRs.
-__device__ __forceinline__ uint32_t tile128_get(u32x32 v0, u32x32 v1, u32x32 v2, u32x32 v3, int r) {
-  const int x = r & 31, q = r >> 5;
-  uint32_t w0 = v0[x], w1 = v1[x], w2 = v2[x], w3 = v3[x];
-  asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
-  const uint32_t a = (q & 1) ? w1 : w0, b = (q & 1) ? w3 : w2;
-  return (q & 2) ? b : a;
-}
-
-template <typename A>
-__device__ __forceinline__ A pick4(const A (&arr)[4], int k) {  // k wave-uniform
-  A x0 = arr[0], x1 = arr[1], x2 = arr[2], x3 = arr[3];
-  asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
-  const A a = (k & 1) ? x1 : x0, b = (k & 1) ? x3 : x2;
-  return (k & 2) ? b : a;
-}
-
-__device__ __forceinline__ int64_t readlane_i64(int64_t x, int l) {
-  return (int64_t)readlane_u64((uint64_t)x, l);
-}
-
-__global__ __launch_bounds__(WAVE, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void santa_sw_kernel(SantaArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int b = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int n = a.n;
-  const SwLds L = sw_lds_layout(a.ng);
-  uint8_t *ltile = smem + L.tile;
-  const uint32_t *ltile32 = (const uint32_t *)ltile;
-  int32_t *rows_l = (int32_t *)(smem + L.rows);
-  int16_t *ctype = (int16_t *)(smem + L.ctype);
-  int32_t *head = (int32_t *)(smem + L.head);
-  int16_t *nxt = (int16_t *)(smem + L.nxt);
-
-  // -- rows, range check, chains ------------------------------------------------
-  int bad = 0;
-  for (int j = lane; j < n; j += WAVE) {
-    const int r = a.rows[(size_t)b * n + j];
-    bad |= (r < 0) || (r >= a.nc);
-    rows_l[j] = r;
-  }
-  if (__any(bad)) {
-    if (lane == 0) atomicOr(a.err, SH_ERRF_ROWS);
-    return;
-  }
-  for (int t = lane; t < a.ng; t += WAVE) head[t] = -1;
-  int badt = 0;
-  for (int j = lane; j < n; j += WAVE) {
-    const int16_t ty = a.types[rows_l[j]];
-    badt |= (ty < 0) || (ty >= a.ng);
-    ctype[j] = ty;
-  }
-  if (__any(badt)) {  // types index LDS tables
-    if (lane == 0) atomicOr(a.err, SH_ERRF_TYPE);
-    return;
-  }
-  __syncthreads();
-  for (int j = lane; j < n; j += WAVE) nxt[j] = (int16_t)atomicExch(&head[ctype[j]], j);
-  __syncthreads();
-
-  // -- build: rows 0..127 staged in the LDS tile area and moved to VGPRs, then
-  //    rows 128..255 built in place (they stay in LDS) -------------------------
-  const int nw = a.n_wish;
-  const int nw1 = nw + 1;
-  u32x32 v0, v1, v2, v3;
-  uint32_t oldcode[4];  // code(row l+64k, column l+64k): the row's own gift
-  {
-    const bool vec = (nw & 3) == 0;
-    const int cpr = vec ? (nw >> 2) : nw;
-    auto put = [&](int lr, int r, int gift) {
-      for (int jj = head[gift]; jj >= 0; jj = nxt[jj])
-        ltile[lr * 256 + (jj & 63) * 4 + (jj >> 6)] = (uint8_t)(r + 1);
-    };
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      const int r0 = g * 128;
-      if (r0 < n) {
-#pragma unroll
-        for (int q = 0; q < 32; ++q) ((uint4 *)ltile)[q * WAVE + lane] = make_uint4(0, 0, 0, 0);
-        __syncthreads();
-        const int rows_here = min(128, n - r0);
-        const int units = rows_here * cpr;
-        if (vec) {
-          constexpr int U = 8;
-          for (int base = 0; base < units; base += WAVE * U) {
-            uint2 q[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const int c = base + u * WAVE + lane;
-              if (c < units) {
-                const int lr = c / cpr, cc = c - lr * cpr;
-                q[u] = *(const uint2 *)(a.wish + (size_t)rows_l[r0 + lr] * nw + 4 * cc);
-              }
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const int c = base + u * WAVE + lane;
-              if (c < units) {
-                const int lr = c / cpr, cc = c - lr * cpr;
-                put(lr, 4 * cc + 0, (int16_t)(q[u].x & 0xFFFFu));
-                put(lr, 4 * cc + 1, (int16_t)(q[u].x >> 16));
-                put(lr, 4 * cc + 2, (int16_t)(q[u].y & 0xFFFFu));
-                put(lr, 4 * cc + 3, (int16_t)(q[u].y >> 16));
-              }
-            }
-          }
-        } else {
-          for (int c = lane; c < units; c += WAVE) {
-            const int lr = c / nw, r = c - lr * nw;
-            put(lr, r, a.wish[(size_t)rows_l[r0 + lr] * nw + r]);
-          }
-        }
-        __syncthreads();
-        // own-gift codes of rows r0 + lane (+64): column lane + 64k, k = 2g, 2g+1
-        oldcode[2 * g] = (ltile32[lane * WAVE + lane] >> (16 * g)) & 0xFFu;
-        oldcode[2 * g + 1] = (ltile32[(lane + 64) * WAVE + lane] >> (16 * g + 8)) & 0xFFu;
-        if (g == 0) {
-#pragma unroll
-          for (int x = 0; x < 32; ++x) {
-            v0[x] = ltile32[x * WAVE + lane];
-            v1[x] = ltile32[(x + 32) * WAVE + lane];
-            v2[x] = ltile32[(x + 64) * WAVE + lane];
-            v3[x] = ltile32[(x + 96) * WAVE + lane];
-          }
-          __syncthreads();
-        }
-      } else {
-        oldcode[2 * g] = oldcode[2 * g + 1] = 0;
-      }
-    }
-  }
-
-// -- solve -----------------------------------------------------------------------
-  const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
-  const int64_t INF = INT64_MAX;
-  int64_t spc[4], nv[4], ur[4];  // ur: u~ of rows lane+64k
-  int path[4], pos[4], r4c[4], c4r[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    nv[k] = 0;
-    ur[k] = 0;
-    path[k] = -1;
-    r4c[k] = -1;
-    c4r[k] = -1;
-  }
-  int64_t steps = 0;
-  int fallbacks = 0;
-  if (a.flags & SH_FLAG_BUILD_ONLY) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) c4r[k] = r4c[k] = lane + WAVE * k;
-  } else {
-    for (int cur = 0; cur < n; ++cur) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int j = lane + WAVE * k;
-        spc[k] = INF;
-        pos[k] = (j < n) ? (n - 1 - j) : -1;
-      }
-      uint32_t vis = ((cur & 63) == lane) ? (1u << (cur >> 6)) : 0u;
-      int nrem = n;
-      int64_t minVal = 0;
-      int i = cur;
-      int sink;
-      for (;;) {
-        ++steps;
-        uint32_t w;
-        if (i < SW_REG_ROWS)
-          w = tile128_get(v0, v1, v2, v3, i);
-        else
-          w = ltile32[(i - SW_REG_ROWS) * WAVE + lane];
-        const int64_t ui = readlane_i64(pick4(ur, i >> 6), i & 63);
-        const uint64_t kb = (uint64_t)KEY_BIAS - (uint64_t)minVal;
-        uint64_t best = ~0ull;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int j = lane + WAVE * k;
-          const int64_t r = single_cost((w >> (8 * k)) & 0xFFu, nw1, a.E) + nv[k] - ui;
-          const bool act = pos[k] >= 0;
-          const bool upd = act && (r < spc[k]);
-          spc[k] = upd ? r : spc[k];
-          path[k] = upd ? i : path[k];
-          const uint32_t lo = (r4c[k] < 0) ? (((uint32_t)(1023 - pos[k]) << 10) | (uint32_t)j)
-                                           : ((1u << 20) | ((uint32_t)pos[k] << 10) | (uint32_t)r4c[k]);
-          const uint64_t key = (key_hi_of((uint64_t)spc[k] + kb) << KEY_LO_BITS) | lo;
-          best = umin64(best, act ? key : ~0ull);
-        }
-        uint64_t g = wave_min_u64_fast(best);
-        // asm results are treated as divergent: make the winner provably uniform
-        g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
-            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
-        const uint64_t hi = g >> KEY_LO_BITS;
-        if (exact || hi == 0 || hi == KEY_HI_MAX) {
-          uint64_t m = ~0ull;
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (pos[k] >= 0) m = umin64(m, (uint64_t)spc[k] ^ SIGN64);
-          m = wave_min_u64_dpp(m);
-          const int64_t ms = (int64_t)(m ^ SIGN64);
-          uint64_t b2 = ~0ull;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int j = lane + WAVE * k;
-            if (pos[k] >= 0 && spc[k] == ms) {
-              const uint32_t lo = (r4c[k] < 0)
-                                      ? (((uint32_t)(1023 - pos[k]) << 10) | (uint32_t)j)
-                                      : ((1u << 20) | ((uint32_t)pos[k] << 10) | (uint32_t)r4c[k]);
-              b2 = umin64(b2, lo);
-            }
-          }
-          g = wave_min_u64_dpp(b2);
-          g = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32)) << 32) |
-              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
-          minVal = ms;
-          ++fallbacks;
-        } else {
-          minVal = minVal + ((int64_t)hi - KEY_BIAS);
-        }
-        const bool assigned = (g >> 20) & 1u;
-        const int pk = (int)((g >> 10) & 1023u);
-        const int aux = (int)(g & 1023u);
-        const int pstar = assigned ? pk : 1023 - pk;
-        const int last = nrem - 1;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int p = pos[k];
-          pos[k] = (p == pstar) ? -1 : ((p == last) ? pstar : p);
-        }
-        --nrem;
-        if (!assigned) {
-          sink = aux;
-          break;
-        }
-        i = __builtin_amdgcn_readfirstlane(aux);
-        if ((i & 63) == lane) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if ((i >> 6) == k) ur[k] -= minVal;
-        }
-        vis |= ((i & 63) == lane) ? (1u << (i >> 6)) : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if ((vis >> k) & 1u) ur[k] += minVal;
-        const int j = lane + WAVE * k;
-        if (j < n && pos[k] < 0) nv[k] = nv[k] + (minVal - spc[k]);
-      }
-      // augment along path[] from the sink back to cur (registers only)
-      int j = sink;
-      for (;;) {
-        const int pi = __builtin_amdgcn_readlane(pick4(path, j >> 6), j & 63);
-        const int t = __builtin_amdgcn_readlane(pick4(c4r, pi >> 6), pi & 63);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (lane + WAVE * k == j) r4c[k] = pi;
-          if (lane + WAVE * k == pi) c4r[k] = j;
-        }
-        j = t;
-        if (pi == cur) break;
-      }
-    }
-  }
-
-  // -- outputs: lane handles rows i = lane + 64k --------------------------------------
-  int64_t cost = 0, dch = 0, dgh = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    // v of column c4r[k] from its owner lane (per-lane source: ds_bpermute)
-    const int col = c4r[k] < 0 ? 0 : c4r[k];
-    int64_t vq[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) vq[q] = __shfl(-nv[q], col & 63, WAVE);
-    const int cs = col >> 6;
-    const int64_t vcol = (cs == 0) ? vq[0] : (cs == 1) ? vq[1] : (cs == 2) ? vq[2] : vq[3];
-    const int i = lane + WAVE * k;
-    if (i < n) {
-      const int64_t cij = ur[k] + vcol;  // = C[i][col] (tight matched edge)
-      const uint32_t cn = (cij == a.E) ? 0u : (uint32_t)((cij >> 32) + nw1);
-      const uint32_t co = oldcode[k];
-      const int child = rows_l[i];
-      const int told = ctype[i], tnew = ctype[col];
-      if (a.flags & SH_FLAG_BUILD_ONLY) {
-        cost += single_cost(co, nw1, a.E);
-      } else {
-        cost += cij;
-        dch += child_happy(cn, nw1) - child_happy(co, nw1);
-        if (a.delta) dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
-      }
-      if (a.col) a.col[(size_t)b * n + i] = col;
-      if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[child] = (int16_t)tnew;  // this block owns child; ctype holds old types
-    }
-  }
-  cost = wave_sum_i64(cost);
-  dch = wave_sum_i64(dch);
-  dgh = wave_sum_i64(dgh);
-  if (lane == 0) {
-    if (a.cost) a.cost[b] = cost;
-    if (a.steps) a.steps[b] = steps;
-    if (a.delta) {
-      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
-      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
     }
     if (fallbacks) atomicAdd(a.err + 1, fallbacks);
   }
@@ -3085,6 +2735,341 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
 }
 
 // ---------------------------------------------------------------------------
+// santa_sp3_kernel: santa_sp2_kernel's design (one wave per block, the hit
+// tile in 64 VGPRs, scipy's SAP decision for decision) with 32-bit values
+// and a 32-bit argmin key.
+//
+// Lattice units.  Every value the solve forms is an integer combination of
+// the two Santa costs: a wish -a * 2^32 and a miss E (units of 2^-31), i.e.
+// x = A * 2^32 + m * E.  While every compared value has |m| <= M with
+// 2M * E < 2^32 (M = 199 at n_wish = 100), comparing x is comparing (A, m)
+// lexicographically, which is comparing the packed integer V = A * 512 + m.
+// So the solve runs on int32 V values (a wish -a * 512, a miss 1) and makes
+// exactly the int64 solve's decisions.  The key of a live column is
+//   (spc_V + 2^20) << 11 | class << 10 | pkey << 2 | k      (one VALU: lshl_or)
+// (class: assigned; pkey: assigned ? pos : 255 - pos; k: the column's slot in
+// its lane), so ONE 32-bit DPP min gives the new minVal, the position that
+// leaves `remaining`, and the winner's lane (the one lane holding the key) and
+// slot; the winner's row comes from a packed byte per column (one readlane).
+// Exactness is checked, not assumed: every row dual a step reads (u~, a
+// scalar) and every column dual after its update (W = -v) stays within
+// |A| <= 1000 / 500 and |m| <= 2M/3 / M/3, which bounds every relaxation value
+// by |A| <= 1627 (inside the 21-bit key field) and |m| <= M; a block that
+// leaves the range is left untouched for the fallback launch (never on the
+// synthetic Kaggle-shaped rounds, where m stays 0 on every dual:
+// tools/analysis/mrange.py; forced in the tests by SH_FLAG_TEST_RANGE).
+// Per step: ~50 VALU (santa_sp2_kernel: 108), no 64-bit LDS traffic.
+// ---------------------------------------------------------------------------
+constexpr int SP3_SH = 11;                  // key tie-break field: class 1 | pkey 8 | k 2
+constexpr int32_t SP3_BIAS = 1 << 20;       // spc_V + BIAS in [0, 2^21) (key field)
+constexpr uint32_t SP3_INF = (1u << 21) - 1u;  // "infinite" spc (never a live winner)
+
+// V = A * 512 + m with |A| <= amax and |m| <= mmax (2 * mmax < 512)
+__device__ __forceinline__ bool sp3_in_range(int32_t V, int amax, int mmax) {
+  return (((uint32_t)(V + mmax) & 511u) <= (uint32_t)(2 * mmax)) &&
+         ((uint32_t)(V + amax * 512 + mmax) <= (uint32_t)(2 * (amax * 512 + mmax)));
+}
+
+struct Sp3Lds {
+  size_t ctype, own, ovfr, ovf, u, rem, rowc, total;
+};
+
+__host__ __device__ __forceinline__ Sp3Lds sp3_lds_layout() {
+  Sp3Lds L;
+  size_t o = 0;
+  L.ctype = o;  o += 256 * 2;                  // column gift types (old)
+  L.own = o;    o += 256;                      // code(i, i): row i's own (old) gift
+  L.ovfr = o;   o += 256 * 4;                  // overflow range per row
+  L.ovf = o;    o += (size_t)SP2_OVF_CAP * 2;  // overflow entries
+  L.u = o;      o += (256 + 64) * 4;           // row duals V (+ a dump slot per lane)
+  L.rem = o;    o += 256;                      // scipy's `remaining`: column at position p
+  L.rowc = o;   o += (256 + 32) * 4;           // current row: C_V per column slot + dump slots
+  L.total = o;
+  return L;
+}
+
+__global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const unsigned char *rec_all) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int n = a.n;
+  const unsigned char *rec = rec_all + (size_t)b * SP2_REC;
+  if (*(const volatile int32_t *)(rec + SP2_REC_STATUS)) return;  // skipped / left to the fallback
+  const Sp3Lds L = sp3_lds_layout();
+  int16_t *ctype = (int16_t *)(smem + L.ctype);
+  uint8_t *own = smem + L.own;
+  uint32_t *ovfr = (uint32_t *)(smem + L.ovfr);
+  uint16_t *ovf = (uint16_t *)(smem + L.ovf);
+  int32_t *u_l = (int32_t *)(smem + L.u);
+  uint8_t *rem = smem + L.rem;
+  int32_t *rowc = (int32_t *)(smem + L.rowc);
+  const int x31 = lane & 31;
+
+  // -- the tile into VGPRs (santa_sp2_kernel's record), the rest to LDS -------------
+  u32x32 T0, T1;
+  {
+    const uint4 *src = (const uint4 *)(rec + SP2_REC_TILE);
+    const int nq4 = (n + 15) >> 4;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      const uint4 v0 = (w < nq4) ? src[w * 64 + lane] : make_uint4(0, 0, 0, 0);
+      const uint4 v1 = (w + 8 < nq4) ? src[(w + 8) * 64 + lane] : make_uint4(0, 0, 0, 0);
+      T0[4 * w + 0] = v0.x; T0[4 * w + 1] = v0.y; T0[4 * w + 2] = v0.z; T0[4 * w + 3] = v0.w;
+      T1[4 * w + 0] = v1.x; T1[4 * w + 1] = v1.y; T1[4 * w + 2] = v1.z; T1[4 * w + 3] = v1.w;
+    }
+    const uint32_t *ro = (const uint32_t *)(rec + SP2_REC_OVF);
+    for (int x = lane; x < SP2_OVF_CAP / 2; x += WAVE) ((uint32_t *)ovf)[x] = ro[x];
+    const uint32_t *rr = (const uint32_t *)(rec + SP2_REC_OVFR);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ovfr[4 * lane + k] = rr[4 * lane + k];
+    ((uint32_t *)own)[lane] = ((const uint32_t *)(rec + SP2_REC_OWN))[lane];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = 4 * lane + k;
+      if (r < n) ctype[r] = a.types[a.rows[(size_t)b * n + r]];
+    }
+  }
+  for (int r = lane; r < n; r += WAVE) u_l[r] = 0;
+  const int nw1 = a.n_wish + 1;
+  const int64_t E = a.E;
+  *(int4 *)(rowc + 4 * lane) = make_int4(1, 1, 1, 1);  // every slot a miss (V = 1)
+  // the lattice bound M (2M * E < 2^32, at most 199 so that |m| fits the packing)
+  const int Mm = (int)min((int64_t)199, (int64_t)(0xFFFFFFFFll / E) / 2);
+  const int mW = (Mm - 1) / 3, mU = Mm - 1 - mW;  // |m(W)| + |m(u~)| + 1 <= M
+  __syncthreads();
+  __builtin_amdgcn_s_setprio(3);  // (lowered over the last Dijkstras, below)
+  const uint64_t m1 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
+
+  uint32_t sb[4];      // spc_V + BIAS (columns 4*lane + k)
+  int32_t W[4];        // -v_V
+  i32x4 path;
+  uint32_t lo[4];      // key tie-break bits; ~0: left `remaining` this Dijkstra (or j >= n)
+  uint32_t c4r = ~0u;  // column of row 4*lane + k in byte k
+  uint32_t r4c = 0;    // row of column 4*lane + k in byte k (valid where assigned)
+  uint64_t AM[4];      // assigned columns (wave masks, SGPRs)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    W[k] = 0;
+    path[k] = -1;
+    AM[k] = 0;
+  }
+  uint32_t rem0 = 0;  // rem[p] = n - 1 - p for this lane's 4 positions
+#pragma unroll
+  for (int k = 0; k < 4; ++k) rem0 |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
+  int steps = 0;
+  bool bad = (a.flags & SH_FLAG_TEST_RANGE) != 0;  // the lattice range left (per-lane flag)
+  uint32_t accm = 0, acca = 0;                     // range of every u~ a step read (see below)
+  const int l4 = 4 * lane;
+  if (a.flags & SH_FLAG_BUILD_ONLY) {
+    c4r = (uint32_t)(4 * lane) * 0x01010101u + 0x03020100u;
+  } else {
+    for (int cur = 0; cur < n; ++cur) {
+      if (cur == n - 32) __builtin_amdgcn_s_setprio(2);  // (santa_sp2_kernel's issue priority)
+      if (cur == n - 8) __builtin_amdgcn_s_setprio(1);
+      if (cur == n - 2) __builtin_amdgcn_s_setprio(0);
+      // Dijkstra set-up: remaining = [n-1 .. 0], every column < n live, spc = inf
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int j = 4 * ln + k;
+        const uint32_t pos = (uint32_t)(n - 1 - j);
+        const bool asg = __builtin_amdgcn_inverse_ballot_w64(AM[k]);
+        const uint32_t pk = asg ? ((1u << 8) | pos) : (255u - pos);
+        lo[k] = (j < n) ? ((pk << 2) | (uint32_t)k) : ~0u;
+        sb[k] = SP3_INF;
+      }
+      ((uint32_t *)rem)[lane] = rem0;
+      int nrem = n;
+      int32_t minVal = 0;
+      int i = cur;
+      int sink;
+      // deferred book-keeping of the previous step: the winner (tie bits pglo,
+      // unique among the live columns) leaves `remaining`, the mover (column
+      // mv) takes its position (tie bits ^= kX)
+      uint32_t pglo = ~0u;
+      int mv = -1;
+      uint32_t kX = 0;
+      for (;;) {
+        ++steps;
+        const uint32_t tw = tile2_get(T0, T1, i >> 2);
+        const int32_t uraw = u_l[i];
+        const int mover_v = rem[nrem - 1];  // the column at the last position
+        const uint32_t e = (tw >> ((i & 1) << 4)) & 0xFFFFu;
+        const uint64_t hmask = ((i >> 1) & 1) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+        const bool mine = __builtin_amdgcn_inverse_ballot_w64(hmask);
+        const uint32_t ea = e >> 9;
+        // book-keeping: the winner first (its tie bits are unique while it is
+        // live; the mover's new bits may equal them), then the mover (a no-op
+        // when the mover is the winner: kX = 0)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          lo[k] = (lo[k] == pglo) ? ~0u : lo[k];
+          lo[k] ^= (l4 + k == mv) ? kX : 0u;
+        }
+        // expand the row: hit columns get -a * 512, the rest hold a miss (1)
+        const int sslot = mine ? (int)(e & 0x1FFu) : 256 + x31;
+        rowc[sslot] = -(int32_t)(ea << 9);
+        // (a row with more than 32 hits: the marker in its entry 31)
+        const bool ovr = __builtin_amdgcn_ballot_w64(mine && ea == SP2_MARK) != 0;
+        if (__builtin_expect(ovr, 0)) {
+          const uint32_t rg = ovfr[i];
+          const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
+          for (int x = lane; x < oc; x += WAVE) {
+            const uint32_t e2 = ovf[os + x];
+            rowc[e2 & 0x1FFu] = -(int32_t)((e2 >> 9) << 9);
+          }
+        }
+        const int2 c01 = *(const int2 *)(rowc + 2 * lane);
+        const int2 c23 = *(const int2 *)(rowc + 128 + 2 * lane);
+        rowc[sslot] = 1;  // un-scatter (in-order LDS: after the reads)
+        if (__builtin_expect(ovr, 0)) {
+          const uint32_t rg = ovfr[i];
+          const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
+          for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = 1;
+        }
+        const int32_t cc[4] = {c01.x, c01.y, c23.x, c23.y};
+        // u~[i] = u[i] - minVal (row i is reached at the current minimum)
+        const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
+        // range of u~ (scalar): the largest m + mU field and the largest |V|
+        accm = max(accm, (uint32_t)(ui + mU) & 511u);
+        acca = max(acca, (uint32_t)(ui < 0 ? -ui : ui));
+        const uint32_t bse = (uint32_t)(SP3_BIAS - ui);
+        uint32_t best = ~0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t r = (uint32_t)W[k] + (uint32_t)cc[k] + bse;
+          // (a removed column never improves: r >= minVal >= its spc)
+          const bool upd = r < sb[k];
+          sb[k] = upd ? r : sb[k];
+          path[k] = upd ? i : path[k];
+          const uint32_t key = (sb[k] << SP3_SH) | lo[k];  // (removed: lo = ~0)
+          best = key < best ? key : best;
+        }
+        const uint32_t g = wave_min_u32_dpp(best);
+        minVal = (int32_t)(g >> SP3_SH) - SP3_BIAS;
+        const int kw = (int)(g & 3u);
+        const uint32_t pkey = (g >> 2) & 255u;
+        const bool assigned = (g >> 10) & 1u;
+        const int lw = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == g));
+        const int pstar = assigned ? (int)pkey : 255 - (int)pkey;
+        const int last = nrem - 1;
+        pglo = g & ((1u << SP3_SH) - 1u);
+        kX = (uint32_t)(last ^ pstar) << 2;
+        mv = mover_v;
+        rem[pstar] = (uint8_t)mover_v;  // (every lane, same byte; a no-op when pstar == last)
+        --nrem;
+        // (branch-free: the row is read either way, used when assigned)
+        const int nxt = (int)((__builtin_amdgcn_readlane((int)r4c, lw) >> (8 * kw)) & 0xFFu);
+        if (!assigned) {
+          sink = 4 * lw + kw;
+          break;
+        }
+        i = nxt;
+      }
+      // Dual update (santa_sp2_kernel's, in V units): the columns that left
+      // `remaining` (lo = ~0; not the sink, whose update is 0) add
+      // minVal - spc to -v and to the dual of their row.
+      const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
+        const int32_t dd = vk ? (int32_t)(mvb - sb[k]) : 0;
+        W[k] += dd;
+        bad |= !sp3_in_range(W[k], 500, mW);
+        const int ua = vk ? (int)((r4c >> (8 * k)) & 0xFFu) : 256 + lane;
+        __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (lane == 0) u_l[cur] += minVal;
+      // augment along path[] from the sink back to cur (registers only)
+      int j = sink;
+      for (;;) {
+        const int jl = j >> 2;
+        const int p0 = __builtin_amdgcn_readlane(path[0], jl), p1 = __builtin_amdgcn_readlane(path[1], jl);
+        const int p2 = __builtin_amdgcn_readlane(path[2], jl), p3 = __builtin_amdgcn_readlane(path[3], jl);
+        const int pi = (j & 2) ? ((j & 1) ? p3 : p2) : ((j & 1) ? p1 : p0);
+        // row pi: its previous column t leaves, j becomes its column
+        const int pl = pi >> 2, ps = 8 * (pi & 3);
+        const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)c4r, pl);
+        const int t = (int)((cw >> ps) & 0xFFu);
+        const uint32_t nw4 = (cw & ~(0xFFu << ps)) | ((uint32_t)j << ps);
+        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(c4r) : "s"(nw4), "{m0}"(pl));
+        // column j: row pi (byte j & 3 of lane j >> 2), now assigned
+        const int js = 8 * (j & 3);
+        const uint32_t rw = (uint32_t)__builtin_amdgcn_readlane((int)r4c, jl);
+        const uint32_t nr4 = (rw & ~(0xFFu << js)) | ((uint32_t)pi << js);
+        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r4c) : "s"(nr4), "{m0}"(jl));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) AM[k] |= ((j & 3) == k) ? 1ull << jl : 0ull;
+        j = t;
+        if (pi == cur) break;
+      }
+    }
+  }
+  __syncthreads();
+
+  {  // the lattice range (see above): leave the block to the fallback launch
+    bool big = bad || accm > (uint32_t)(2 * mU) || acca > (uint32_t)(1000 * 512 + mU);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (4 * lane + k < n) big |= !sp3_in_range(u_l[4 * lane + k], 1000, mU);
+    if (__builtin_expect(__any(big), 0)) {
+      if (lane == 0) {
+        const int p = atomicAdd(a.ovf_cnt, 1);
+        a.ovf_list[p] = b;
+      }
+      return;
+    }
+  }
+  const uint64_t m2 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
+  // -- outputs: lane handles rows i = 4*lane + k ------------------------------------
+  int64_t cost = 0, dch = 0, dgh = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = 4 * lane + k;
+    const int col = (int)((c4r >> (8 * k)) & 0xFFu);
+    int32_t vq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vq[q] = __shfl(-W[q], col >> 2, WAVE);
+    const int cs = col & 3;
+    const int32_t vcol = (cs == 0) ? vq[0] : (cs == 1) ? vq[1] : (cs == 2) ? vq[2] : vq[3];
+    if (i < n) {
+      const uint32_t co = own[i];
+      const int chd = a.rows[(size_t)b * n + i];
+      const int told = ctype[i], tnew = ctype[col];
+      if (a.flags & SH_FLAG_BUILD_ONLY) {
+        cost += single_cost(co, nw1, E);
+      } else {
+        // C_V = u + v on the matched (tight) edge: a miss (A 0, m 1) or a wish (-a, 0)
+        const int32_t cv = u_l[i] + vcol;
+        const int32_t mc = ((cv + 256) & 511) - 256;
+        const int32_t ac = (cv - mc) >> 9;
+        const int64_t cij = (int64_t)ac * 4294967296LL + (int64_t)mc * E;
+        const uint32_t cn = mc ? 0u : (uint32_t)(ac + nw1);
+        cost += cij;
+        dch += child_happy(cn, nw1) - child_happy(co, nw1);
+        if (a.delta) dgh += gift_happy(a, chd, tnew) - gift_happy(a, chd, told);
+      }
+      if (a.col) a.col[(size_t)b * n + i] = col;
+      if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[chd] = (int16_t)tnew;  // this block owns chd
+    }
+  }
+  cost = wave_sum_i64(cost);
+  dch = wave_sum_i64(dch);
+  dgh = wave_sum_i64(dgh);
+  if (lane == 0) {
+    if (a.cost) a.cost[b] = cost;
+    if (a.steps) a.steps[b] = steps;
+    if ((a.flags & SH_FLAG_TIMING) && a.col && n > 1)  // solve, shader cycles
+      a.col[(size_t)b * n + 1] = (int32_t)min(m2 - m1, (uint64_t)INT32_MAX);
+    if (a.delta) {
+      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
+      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Large-block Santa kernel (256 < n <= 4096, both modes): the reference's own
 // block sizes (2000 singles, mpi_single.py:238; 3000 pairs, mpi_twins.py:244).
 //
@@ -3813,13 +3798,6 @@ int launch_santa(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
-int launch_santa_sw(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
-  const SwLds L = sw_lds_layout(ctx->ng);
-  if (L.total > 64 * 1024) return fail(SH_ERR_ARGS, "too many gift types for the LDS chain heads");
-  hipLaunchKernelGGL(santa_sw_kernel, dim3(B), dim3(WAVE), L.total, s, a);
-  HIP_TRY(hipGetLastError());
-  return SH_OK;
-}
 
 template <int MODE, bool SC = false>
 int launch_santa_vt(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
@@ -3846,30 +3824,45 @@ int launch_big_cfg(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) 
   return SH_OK;
 }
 
-template <int MODE>
-int launch_santa_big(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
-  const int n = a.n;
-  // A full round (at least one block per CU: 477 blocks at n = 2000) runs
-  // four columns per thread, so ceil(n / 256) waves per block -- fewer waves
-  // per SIMD competing for issue between each block's barriers than 16: n =
-  // 2000 round 0 113 -> 78 ms (8 waves; 4 waves x 8 columns: 93 ms), n = 1024
-  // 101 -> 30 ms and n = 600 76 -> 21 ms (4 waves); the row rebuild takes one
-  // thread per wish of a unit, (MODE + 1) * n_wish <= NW * 64.  A few blocks
-  // (twins at 3000 pairs: 6 per round, triplets) keep the wider blocks (a
-  // lone n = 2000 block: 52 ms at 16 waves, 55 at 8).
-  // (profiles/r02c_big_rowbuild_ab.jsonl, profiles/r02c_big_nw_ab.jsonl)
+template <int NW_, int K_, int FB_>
+struct BigCfg {
+  static constexpr int NW = NW_, K = K_, FB = FB_;
+};
+
+// The santa_big_kernel configuration of a launch of B blocks of n rows, handed
+// to f as a BigCfg<NW, K, FB> tag: one picker for the launch and for its
+// occupancy (sh_resident_blocks), so the two cannot drift.
+// A full round (at least one block per CU: 477 blocks at n = 2000) runs
+// four columns per thread, so ceil(n / 256) waves per block -- fewer waves
+// per SIMD competing for issue between each block's barriers than 16: n =
+// 2000 round 0 113 -> 78 ms (8 waves; 4 waves x 8 columns: 93 ms), n = 1024
+// 101 -> 30 ms and n = 600 76 -> 21 ms (4 waves); the row rebuild takes one
+// thread per wish of a unit, (MODE + 1) * n_wish <= NW * 64.  A few blocks
+// (twins at 3000 pairs: 6 per round, triplets) keep the wider blocks (a
+// lone n = 2000 block: 52 ms at 16 waves, 55 at 8).
+// (profiles/r02c_big_rowbuild_ab.jsonl, profiles/r02c_big_nw_ab.jsonl)
+template <int MODE, typename F>
+int with_big_cfg(const sh_ctx *ctx, int n, int B, F &&f) {
   const bool many = B >= ctx->n_cu;
   if constexpr (MODE == 0) {
-    if (many && n <= 512) return launch_big_cfg<MODE, 2, 4, 10>(ctx, a, B, s);
+    if (many && n <= 512) return f(BigCfg<2, 4, 10>{});
   }
   if constexpr (MODE <= 1) {
-    if (many && n > 512 && n <= 1024) return launch_big_cfg<MODE, 4, 4, 10>(ctx, a, B, s);
+    if (many && n > 512 && n <= 1024) return f(BigCfg<4, 4, 10>{});
   }
-  if (n <= 512) return launch_big_cfg<MODE, 8, 1, 10>(ctx, a, B, s);
-  if (n <= 1024) return launch_big_cfg<MODE, 16, 1, 10>(ctx, a, B, s);
-  if (n <= 2048) return many ? launch_big_cfg<MODE, 8, 4, 12>(ctx, a, B, s) : launch_big_cfg<MODE, 16, 2, 12>(ctx, a, B, s);
-  if (n <= 3072) return launch_big_cfg<MODE, 16, 3, 12>(ctx, a, B, s);
-  return launch_big_cfg<MODE, 16, 4, 12>(ctx, a, B, s);
+  if (n <= 512) return f(BigCfg<8, 1, 10>{});
+  if (n <= 1024) return f(BigCfg<16, 1, 10>{});
+  if (n <= 2048) return many ? f(BigCfg<8, 4, 12>{}) : f(BigCfg<16, 2, 12>{});
+  if (n <= 3072) return f(BigCfg<16, 3, 12>{});
+  return f(BigCfg<16, 4, 12>{});
+}
+
+template <int MODE>
+int launch_santa_big(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
+  return with_big_cfg<MODE>(ctx, a.n, B, [&](auto c) {
+    using C = decltype(c);
+    return launch_big_cfg<MODE, C::NW, C::K, C::FB>(ctx, a, B, s);
+  });
 }
 
 // The overflow lists of the designs with a fallback launch (block ids, two
@@ -3947,8 +3940,11 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
     if (a.flags & SH_FLAG_EXACT_ARGMIN)
       hipLaunchKernelGGL(santa_sp2_kernel<true>, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
                          (const unsigned char *)ctx->d_rec);
-    else
+    else if (a.flags & SH_FLAG_SP2)
       hipLaunchKernelGGL(santa_sp2_kernel<false>, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
+                         (const unsigned char *)ctx->d_rec);
+    else
+      hipLaunchKernelGGL(santa_sp3_kernel, dim3(B), dim3(WAVE), sp3_lds_layout().total, s, a,
                          (const unsigned char *)ctx->d_rec);
   } else if (vec)
     hipLaunchKernelGGL(santa_sp_kernel<true>, dim3(B), dim3(WAVE), lds, s, a);
@@ -4008,13 +4004,15 @@ int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
   if (mode == SH_MODE_TWINS) return SH_DESIGN_TWINS;
   if (flags & SH_FLAG_LDS_TILE) return SH_DESIGN_LDS_TILE;
-  if (flags & SH_FLAG_SW_TILE) return SH_DESIGN_SW_TILE;
+  // (SH_FLAG_SW_TILE, the retired one-wave register-tile kernel, is refused
+  // by the entry points)
   // the sparse kernel packs child ids (< 2^20) and gift types (< 1023) in one
   // dword during its build; other instances take the register-tile kernel
   if ((flags & SH_FLAG_VT_TILE) || ctx->nc > (1 << 20) || ctx->ng > 1022) return SH_DESIGN_VT_TILE;
   // the register-tile sparse kernel keeps the wish value in 7 bits with one
   // code reserved (n_wish <= 126); the LDS-list kernel takes the rest
-  const int sparse = (ctx->n_wish <= 126 && !(flags & SH_FLAG_SP1)) ? SH_DESIGN_SPARSE2 : SH_DESIGN_SPARSE;
+  const int sparse = (ctx->n_wish > 126 || (flags & SH_FLAG_SP1)) ? SH_DESIGN_SPARSE
+                     : (flags & (SH_FLAG_SP2 | SH_FLAG_EXACT_ARGMIN)) ? SH_DESIGN_SPARSE2 : SH_DESIGN_SPARSE3;
   if (flags & (SH_FLAG_SP_TILE | SH_FLAG_SP1)) return sparse;
   // few blocks (at most one resident wave of LDS-tile blocks): every block
   // starts at once and the launch takes one block's latency, which the
@@ -4025,7 +4023,7 @@ int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   // latency-bound shard of a round at 4 GPUs (933 blocks: 1.68 vs 2.13 ms at
   // round 0, 0.67 vs 0.89 ms at round 10 for the sparse kernel; beyond it the
   // sparse kernel's 4 blocks per SIMD win: 1865 blocks 2.45 vs 2.76 ms)
-  if (sparse == SH_DESIGN_SPARSE2 && B <= vt_tile_slots(ctx)) return SH_DESIGN_VT_TILE;
+  if (sparse != SH_DESIGN_SPARSE && B <= vt_tile_slots(ctx)) return SH_DESIGN_VT_TILE;
   return sparse;
 }
 
@@ -4041,28 +4039,25 @@ int occ_blocks(const sh_ctx *ctx, F f, int threads, size_t lds) {
 }
 
 template <int MODE>
-int big_resident(const sh_ctx *ctx, int n) {  // mirrors launch_santa_big's configurations
-#define BR_(NW, K, FB) \
-  return occ_blocks(ctx, santa_big_kernel<MODE, NW, K, FB>, NW * WAVE, big_lds_layout(n, MODE, ctx->ng, NW, K).total)
-  if (n <= 512) BR_(8, 1, 10);
-  if (n <= 1024) BR_(16, 1, 10);
-  if (n <= 2048) BR_(16, 2, 12);
-  if (n <= 3072) BR_(16, 3, 12);
-  BR_(16, 4, 12);
-#undef BR_
+int big_resident(const sh_ctx *ctx, int n, int B) {  // the configuration launch_santa_big picks
+  return with_big_cfg<MODE>(ctx, n, B, [&](auto c) {
+    using C = decltype(c);
+    return occ_blocks(ctx, santa_big_kernel<MODE, C::NW, C::K, C::FB>, C::NW * WAVE,
+                      big_lds_layout(n, MODE, ctx->ng, C::NW, C::K).total);
+  });
 }
 
-int resident_blocks(sh_ctx *ctx, int design, int mode, int n) {
+int resident_blocks(sh_ctx *ctx, int design, int mode, int n, int B) {
   switch (design) {
     case SH_DESIGN_LARGE:
-      return mode == SH_MODE_SINGLE ? big_resident<0>(ctx, n)
-             : mode == SH_MODE_TWINS ? big_resident<1>(ctx, n) : big_resident<2>(ctx, n);
+      return mode == SH_MODE_SINGLE ? big_resident<0>(ctx, n, B)
+             : mode == SH_MODE_TWINS ? big_resident<1>(ctx, n, B) : big_resident<2>(ctx, n, B);
     case SH_DESIGN_TWINS:
       return occ_blocks(ctx, santa_block_kernel<1, 1>, SANTA_WG, santa_lds_layout(n, 1, ctx->ng).total);
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
-    case SH_DESIGN_SW_TILE: return occ_blocks(ctx, santa_sw_kernel, WAVE, sw_lds_layout(ctx->ng).total);
     case SH_DESIGN_VT_TILE: return vt_tile_slots(ctx);
     case SH_DESIGN_SPARSE2: return occ_blocks(ctx, santa_sp2_kernel<false>, WAVE, sp2_lds_layout().total);
+    case SH_DESIGN_SPARSE3: return occ_blocks(ctx, santa_sp3_kernel, WAVE, sp3_lds_layout().total);
     default:
       return occ_blocks(ctx, santa_sp_kernel<true>, WAVE, sp_lds_layout(ctx->ng, sp_capacity(ctx)).total);
   }
@@ -4080,6 +4075,7 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   if (n <= 0 || n > SH_MAX_N_SANTA) return fail(SH_ERR_ARGS, "n must be in [1, 4096]");
   if ((int64_t)n * (mode + 1) > ctx->nc) return fail(SH_ERR_ARGS, "block larger than the instance");
   if (B < 0) return fail(SH_ERR_ARGS, "B < 0");
+  if (flags & SH_FLAG_SW_TILE) return fail(SH_ERR_ARGS, "SH_FLAG_SW_TILE: the one-wave register-tile design is retired");
   if (B == 0) return SH_OK;
   DeviceGuard dg(ctx->device);
   SantaArgs a;
@@ -4097,9 +4093,9 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
                                      : launch_santa_big<2>(ctx, a, B, s);
     case SH_DESIGN_TWINS: return launch_santa<1, 1>(ctx, a, B, s);
     case SH_DESIGN_LDS_TILE: return launch_santa<1, 0>(ctx, a, B, s);
-    case SH_DESIGN_SW_TILE: return launch_santa_sw(ctx, a, B, s);
     case SH_DESIGN_VT_TILE: return launch_santa_vt_sc(ctx, a, B, s);
-    case SH_DESIGN_SPARSE2: return launch_santa_sp(ctx, a, B, s, true);
+    case SH_DESIGN_SPARSE2:
+    case SH_DESIGN_SPARSE3: return launch_santa_sp(ctx, a, B, s, true);
     default: return launch_santa_sp(ctx, a, B, s, false);
   }
 }
@@ -4109,6 +4105,7 @@ int sh_solve_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS && mode != SH_MODE_TRIPLETS)
     return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA || B < 0) return fail(SH_ERR_ARGS, "bad n or B");
+  if (flags & SH_FLAG_SW_TILE) return fail(SH_ERR_ARGS, "SH_FLAG_SW_TILE: the one-wave register-tile design is retired");
   DeviceGuard dg(ctx->device);
   return pick_design(ctx, mode, n, B, flags);
 }
@@ -4119,7 +4116,8 @@ int sh_resident_blocks(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
     return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA || B < 0) return fail(SH_ERR_ARGS, "bad n or B");
   DeviceGuard dg(ctx->device);
-  return resident_blocks(ctx, pick_design(ctx, mode, n, B, flags), mode, n);
+  if (flags & SH_FLAG_SW_TILE) return fail(SH_ERR_ARGS, "SH_FLAG_SW_TILE: the one-wave register-tile design is retired");
+  return resident_blocks(ctx, pick_design(ctx, mode, n, B, flags), mode, n, B);
 }
 
 int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream) {

@@ -121,11 +121,73 @@ def exchange(engine, world: World, mode: int, rows: torch.Tensor, n: int, B: int
     engine.unpack_types(types, rows[:B * n], recv[:B * n], mode)
 
 
+def check_engine_errors(engine) -> None:
+    """Raise if the device flagged a skipped block since the last check (an
+    out-of-range child id or gift type, an infeasible solve: the kernels
+    leave such a block's types unchanged, which would otherwise be scored
+    and accepted silently).  Synchronises the engine's stream."""
+    read = getattr(engine, "error_flags", None)
+    flags = read() if read is not None else 0
+    if flags:
+        raise RuntimeError(f"sh_solve_blocks skipped blocks (device error flags {flags:#x}: "
+                           "1 = child id out of range, 2 = infeasible, 4 = gift type out of range)")
+
+
+class _Sums:
+    """Where a round's (S_child, S_gift) come from.
+
+    full (check_every == 0): a rescore of the whole state every round, as the
+    reference does on every rank (mpi_single.py:157).
+    delta (check_every = K > 0; the default at N > 1): every
+    rank's block kernels add the exact happiness deltas of ITS blocks into an
+    int64[2], one all-reduce(sum) of those 16 bytes (RCCL over xGMI) gives the
+    round's delta, and S = S(start state of the round) + delta; a full rescore
+    of the state every K rounds (and after the last round) must agree, or the
+    run stops with an error.  Integer sums: order-free, bit-exact."""
+
+    def __init__(self, engine, world: World, check_every: int | None, max_rounds: int):
+        if check_every is None:
+            check_every = 16 if world.distributed else 0
+        self.every = int(check_every) if hasattr(engine, "delta_begin") else 0
+        self.engine, self.world, self.max_rounds = engine, world, max_rounds
+        self.bufs = [engine.new_delta() for _ in range(2)] if self.every else None
+
+    @property
+    def delta(self) -> bool:
+        return self.every > 0
+
+    def check_round(self, rnd: int) -> bool:
+        return (rnd + 1) % self.every == 0 or rnd == self.max_rounds - 1
+
+    def buffer(self, k: int):
+        d = self.bufs[k]
+        d.zero_()
+        return d
+
+    def reduce(self, d) -> None:
+        if self.world.distributed:
+            import torch.distributed as dist
+            dist.all_reduce(d, group=self.world.group)
+
+    @staticmethod
+    def combine(base, rnd, dc, dg, full):
+        """(S_child, S_gift, bad_triplets, bad_twins) of the round's state from
+        the start state's sums and the all-reduced delta (checked against the
+        full rescore when one was taken)."""
+        sc, sg = base[0] + dc, base[1] + dg
+        if full is None:
+            return sc, sg, 0, 0
+        if (full[0], full[1]) != (sc, sg):
+            raise RuntimeError(f"round {rnd}: delta sums ({sc}, {sg}) != full rescore ({full[0]}, {full[1]})")
+        return full
+
+
 def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, n: int = 256,
                blocks_per_round: int | None = None, seed: int = 2017, max_rounds: int = 100,
                accept: str | None = None, patience: int = 3, world: World | None = None,
-               on_round=None, score0: float | None = None,
-               check_disjoint: bool = False, pipeline: bool = False) -> LoopResult:
+               on_round=None, score0: float | None = None, sums0: tuple | None = None,
+               check_disjoint: bool = False, pipeline: bool = False,
+               score_check_every: int | None = None) -> LoopResult:
     """The reference's while-loop; `types` (device int16 [nc]) is updated in place.
 
     accept: "always" (mpi_single.py: the new state is always kept) or
@@ -137,7 +199,12 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
     score_begin; keep-if-improved rounds are speculated and re-run after a
     rejection); identical results and history, but `types`
     already holds round r+1 when on_round(r) runs, so an on_round that reads
-    the state (a checkpoint) needs the serial loop."""
+    the state (a checkpoint) needs the serial loop.
+    score_check_every: 0 = rescore the whole state every round (the
+    reference); K > 0 = the delta all-reduce of SURVEY §8(e) with a full
+    rescore every K rounds that must agree (see _Sums); default K = 16 at
+    N > 1 and 0 on one rank.  sums0: the exact (S_child, S_gift) of the
+    start state, if known (else one rescore)."""
     world = world or World()
     accept = accept or ("always" if mode == _lib.SH_MODE_SINGLE else "improve")
     if accept not in ("always", "improve"):
@@ -151,9 +218,12 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
         raise ValueError(f"{world.size} ranks > {nb} twin blocks per round (the reference "
                          "raises IndexError at mpi_twins.py:132)")
     res = LoopResult()
+    sums = _Sums(engine, world, score_check_every, max_rounds)
+    if sums0 is None and (score0 is None or sums.delta):
+        sums0 = tuple(engine.score_sums(types)[:2])
     if score0 is None:
-        sc, sg, _, _ = engine.score_sums(types)
-        score0 = engine.score_from_sums(sc, sg)
+        score0 = engine.score_from_sums(*sums0)
+    cur = sums0  # exact sums of the current (accepted) state, delta mode
     best = score0
     res.best_score = best
     count = 0
@@ -161,8 +231,10 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
     backup = torch.empty_like(types) if accept == "improve" else None
     b0, b1, _ = shard_range(B, world.rank, world.size)
     if pipeline and hasattr(engine, "score_begin"):
-        return _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
-                              on_round, best, check_disjoint, res, accept)
+        res = _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
+                             on_round, best, check_disjoint, res, accept, sums, cur)
+        check_engine_errors(engine)
+        return res
     for rnd in range(max_rounds):
         t0 = time.perf_counter()
         rows = engine.sample_blocks(mode, n, B, seed, rnd)
@@ -170,11 +242,19 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
             assert_disjoint(rows, mode)
         if backup is not None:
             backup.copy_(types)
+        d = sums.buffer(0) if sums.delta else None
         if b1 > b0:
-            engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types)
+            engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types, delta=d)
         if world.distributed:
             exchange(engine, world, mode, rows, n, B, types, buffers)
-        sc, sg, bad_tri, bad_tw = engine.score_sums(types)
+        if check_disjoint:
+            check_engine_errors(engine)
+        if sums.delta:
+            sums.reduce(d)
+            sc, sg, bad_tri, bad_tw = sums.combine(
+                cur, rnd, *engine.delta_begin(types, d, sums.check_round(rnd)).result())
+        else:
+            sc, sg, bad_tri, bad_tw = engine.score_sums(types)
         if bad_tri or bad_tw:
             raise AssertionError("triplets/twins must share a gift (mpi_single.py:32-44)")
         score = engine.score_from_sums(sc, sg)
@@ -188,6 +268,8 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
         if accept == "improve" and not improved:
             types.copy_(backup)
             kept = False
+        if kept:
+            cur = (sc, sg)
         res.rounds += 1
         res.blocks_solved += B
         st = RoundStats(rnd, sc, sg, score, kept, best, B, time.perf_counter() - t0)
@@ -197,11 +279,12 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
         if count > patience:
             break
     res.best_score = best
+    check_engine_errors(engine)
     return res
 
 
 def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world, on_round, best,
-                   check_disjoint, res: LoopResult, accept: str = "always") -> LoopResult:
+                   check_disjoint, res: LoopResult, accept: str, sums: _Sums, cur) -> LoopResult:
     """run_rounds with round r's score overlapped with round r+1 (see the
     module docstring); same decisions, history and final state as the serial
     loop.  Round r+1 is launched speculatively from round r's result.  When
@@ -223,10 +306,16 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
         rows = engine.sample_blocks(mode, n, B, seed, r)
         if check_disjoint:
             assert_disjoint(rows, mode)
+        d = sums.buffer(k) if sums.delta else None
         if b1 > b0:
-            engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types)
+            engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types, delta=d)
         if world.distributed:
             exchange(engine, world, mode, rows, n, B, types, buffers)
+        if check_disjoint:
+            check_engine_errors(engine)
+        if sums.delta:
+            sums.reduce(d)
+            return engine.delta_begin(types, d, sums.check_round(r))
         return engine.score_begin(types)
 
     while True:
@@ -239,7 +328,10 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
             handle = launch(rnd, k)
         if pending is not None:
             prnd, ph, pt0, pk = pending
-            sc, sg, bad_tri, bad_tw = ph.result()
+            if sums.delta:  # (a rejected round's successor re-runs from the same start state)
+                sc, sg, bad_tri, bad_tw = sums.combine(cur, prnd, *ph.result())
+            else:
+                sc, sg, bad_tri, bad_tw = ph.result()
             if bad_tri or bad_tw:
                 raise AssertionError("triplets/twins must share a gift (mpi_single.py:32-44)")
             score = engine.score_from_sums(sc, sg)
@@ -252,6 +344,8 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
             kept = improved or not improve
             if not kept:
                 types.copy_(pre[pk])  # the state after round prnd is its starting state
+            else:
+                cur = (sc, sg)
             res.rounds += 1
             res.blocks_solved += B
             st = RoundStats(prnd, sc, sg, score, kept, best, B, t0 - pt0)
@@ -294,8 +388,11 @@ class GPUEngine:
     def sample_blocks(self, mode, n, B, seed, rnd):
         return self.ctx.sample_blocks(mode, n, B, seed, rnd)
 
-    def solve_blocks(self, mode, rows, n, types):
-        self.ctx.solve_blocks(mode, rows, n, types)
+    def solve_blocks(self, mode, rows, n, types, delta=None):
+        self.ctx.solve_blocks(mode, rows, n, types, delta=delta)
+
+    def new_delta(self):
+        return torch.zeros(2, dtype=torch.int64, device=self.ctx.device)
 
     def pack_types(self, types, rows, out):
         self.ctx.pack_types(types, rows, out)
@@ -306,16 +403,29 @@ class GPUEngine:
     def score_sums(self, types):
         return self.ctx.score_sums(types)
 
+    def error_flags(self):
+        return self.ctx.error_flags()
+
     def score_begin(self, types):
         """Snapshot `types` and score the snapshot on a side stream; returns a
         handle with result() -> score sums and restore(types) -> copy the
         snapshot back (pipelined rounds)."""
+        return self._begin(types, None, True)
+
+    def delta_begin(self, types, d, full: bool):
+        """Delta rounds: snapshot `types`, copy the (all-reduced) delta d to
+        the host and, if `full`, rescore the snapshot on the side stream;
+        result() -> (dS_child, dS_gift, full sums or None)."""
+        return self._begin(types, d, full)
+
+    def _begin(self, types, d, full: bool):
         if not hasattr(self, "_side"):
             dev = types.device
             self._side = torch.cuda.Stream(dev)
             self._snaps = [torch.empty_like(types) for _ in range(2)]
             self._sums = [torch.zeros(4, dtype=torch.int64, device=dev) for _ in range(2)]
             self._host = [torch.zeros(4, dtype=torch.int64).pin_memory() for _ in range(2)]
+            self._dhost = [torch.zeros(2, dtype=torch.int64).pin_memory() for _ in range(2)]
             self._done = [None, None]
             self._k = 0
         k = self._k
@@ -325,22 +435,32 @@ class GPUEngine:
             main.wait_event(self._done[k])  # the score two rounds back has read the snapshot
         snap = self._snaps[k]
         snap.copy_(types)
+        dhost = self._dhost[k]
+        if d is not None:
+            dhost.copy_(d, non_blocking=True)
         ready = torch.cuda.Event()
         ready.record(main)
-        side = self._side
-        with torch.cuda.stream(side):
-            side.wait_event(ready)
-            self.ctx.score_sums_async(snap, out=self._sums[k])
-            self._host[k].copy_(self._sums[k], non_blocking=True)
-            done = torch.cuda.Event()
-            done.record(side)
+        done = ready
+        if full:
+            side = self._side
+            with torch.cuda.stream(side):
+                side.wait_event(ready)
+                self.ctx.score_sums_async(snap, out=self._sums[k])
+                self._host[k].copy_(self._sums[k], non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(side)
         self._done[k] = done
         host = self._host[k]
 
         class _Handle:
             def result(_):
+                if d is not None:
+                    ready.synchronize()
                 done.synchronize()
-                return tuple(int(x) for x in host.tolist())
+                sums = tuple(int(x) for x in host.tolist()) if full else None
+                if d is None:
+                    return sums
+                return int(dhost[0]), int(dhost[1]), sums
 
             def restore(_, t):
                 torch.cuda.current_stream(t.device).wait_event(done)

@@ -43,7 +43,8 @@ def solve_batched(C: torch.Tensor, with_cost: bool = True, flags: int = 0):
     L = _lib.lib()
     fl = _lib.SH_COMPAT_TIEBREAK | flags
     if C.dtype == torch.int64:
-        if C.numel() and int(C.abs().max()) >= INT64_COST_LIMIT:
+        # (max / -min as Python ints: abs() wraps at INT64_MIN)
+        if C.numel() and max(int(C.max()), -int(C.min())) >= INT64_COST_LIMIT:
             raise ValueError("int64 costs must satisfy |C| < 2**50; pass float64 instead")
         cost = torch.empty(B, dtype=torch.int64, device=dev) if with_cost else None
         rc = L.lsap_solve_batched_i64(_p(C), n, B, _p(col), _p(cost), fl, s)
@@ -96,18 +97,20 @@ def linear_sum_assignment(cost_matrix, maximize: bool = False, device: int | str
         # negating an unsigned array wraps: widen first (uint64 beyond int64 -> float64)
         C = C.astype(np.int64) if (C.size == 0 or int(C.max()) <= np.iinfo(np.int64).max) \
             else C.astype(np.float64)
-    if maximize:
-        C = -C
     # scipy solves in float64.  Integer input is solved in exact int64, which
     # makes scipy's decisions only while every value it forms is an integer
     # below 2^53 (no float64 rounding); duals and path lengths stay within a few
-    # n * max|C|, so 4 (n + 1) max|C| < 2^53 is a safe bound.
+    # n * max|C|, so 4 (n + 1) max|C| < 2^53 is a safe bound.  The bound is
+    # taken in Python ints before any negation (np.abs / -C wrap at INT64_MIN).
     # Wider ranges take the float64 replay of scipy's own arithmetic.
     if np.issubdtype(C.dtype, np.integer) and \
-            (C.size == 0 or 4 * (n + 1) * int(np.abs(C.astype(np.int64)).max()) < EXACT_INT_LIMIT):
-        Ct = torch.from_numpy(np.ascontiguousarray(C, dtype=np.int64)).to(dev)
+            (C.size == 0 or 4 * (n + 1) * max(int(C.max()), -int(C.min())) < EXACT_INT_LIMIT):
+        Ci = np.ascontiguousarray(C, dtype=np.int64)
+        Ct = torch.from_numpy(-Ci if maximize else Ci).to(dev)
     else:
         Cf = np.ascontiguousarray(C, dtype=np.float64)
+        if maximize:
+            Cf = -Cf
         if np.isnan(Cf).any() or np.isneginf(Cf).any():
             raise ValueError("matrix contains invalid numeric entries")
         Ct = torch.from_numpy(Cf).to(dev)

@@ -43,9 +43,30 @@ class CPUOracleEngine:
         lo, count, stride, _ = self.geometry(mode, n)
         return torch.from_numpy(sample_blocks(seed, rnd, lo, count, stride, n, B).reshape(-1).copy())
 
-    def solve_blocks(self, mode, rows, n, types):
+    def solve_blocks(self, mode, rows, n, types, delta=None):
         t = types.numpy()
+        s0 = oracle.score_sums(self.wish, self.good, t) if delta is not None else None
         oracle.round_blocks(mode, self.wish, t, rows.numpy().reshape(-1, n), ng=self.ng)
+        if delta is not None:  # only this engine's blocks changed in between
+            s1 = oracle.score_sums(self.wish, self.good, t)
+            delta += torch.tensor([s1[0] - s0[0], s1[1] - s0[1]], dtype=torch.int64)
+
+    def new_delta(self):
+        return torch.zeros(2, dtype=torch.int64)
+
+    def delta_begin(self, types, d, full):
+        """Delta-round protocol (GPUEngine.delta_begin)."""
+        snap = types.clone()
+        eng = self
+        dv = (int(d[0]), int(d[1]))
+
+        class _Handle:
+            def result(_):
+                return dv[0], dv[1], (eng.score_sums(snap) if full else None)
+
+            def restore(_, t):
+                t.copy_(snap)
+        return _Handle()
 
     def pack_types(self, types, rows, out):
         r = rows.numpy()

@@ -37,6 +37,7 @@ def rank_main(rank, size, port, mode, n, rounds, seed, out):
 
         res = run_rounds(Rec(ctx), types, mode=mode, n=n, seed=seed, max_rounds=rounds,
                          patience=100, world=World(rank, size, None))
-        out[rank] = (types.cpu().numpy(), sums, [st.score for st in res.history], ctx.error_flags())
+        out[rank] = (types.cpu().numpy(), [(st.s_child, st.s_gift) for st in res.history],
+                     [st.score for st in res.history], ctx.error_flags(), sums)
     finally:
         dist.destroy_process_group()

@@ -151,31 +151,43 @@ def test_pipelined_rounds_equal_serial(mode, n, accept, warm, patience, rounds):
     if warm:  # a converged state, where keep-if-improved rounds get rejected
         run_rounds(CPUOracleEngine(sd.wish, sd.goodkids, sd.nq), start, mode=mode, n=n, seed=99,
                    max_rounds=warm, patience=100, world=World())
+    r0, _ = _serial_vs_pipelined(sd, start, mode, n, accept, patience, rounds)
+    if patience == -1:
+        assert r0 == 1  # stopped after the first round; the speculative second was undone
+
+
+def _serial_vs_pipelined(sd, start, mode, n, accept, patience, rounds):
+    """Run both loops from `start`; assert identical state, history and
+    counts; return (rounds run, whether any round was rejected)."""
+    from cpu_engine import CPUOracleEngine
     out = []
-    seen = []
     for pipeline in (False, True):
         eng = CPUOracleEngine(sd.wish, sd.goodkids, sd.nq)
         t = start.clone()
         res = run_rounds(eng, t, mode=mode, n=n, seed=5, max_rounds=rounds, accept=accept,
                          patience=patience, world=World(), pipeline=pipeline)
         hist = [(st.round, st.s_child, st.s_gift, st.score, st.accepted, st.best) for st in res.history]
-        seen.append(any(not st.accepted for st in res.history))
         out.append((t.numpy().copy(), hist, res.rounds, res.blocks_solved, res.best_score))
     (t0, h0, r0, b0, s0), (t1, h1, r1, b1, s1) = out
     assert np.array_equal(t0, t1)
     assert h0 == h1 and r0 == r1 and b0 == b1 and s0 == s1
-    if patience == -1:
-        assert r0 == 1  # stopped after the first round; the speculative second was undone
-    rejected_rounds_seen.append(seen[0])
+    return r0, any(not a for (_, _, _, _, a, _) in h0)
 
 
-rejected_rounds_seen = []
-
-
-def test_pipelined_rejections_were_exercised():
-    """(the keep-if-improved cases above must include rejected rounds, so the
-    re-run path of the pipelined loop was compared with the serial loop)"""
-    assert any(rejected_rounds_seen)
+@pytest.mark.parametrize("warm", [12, 40])
+def test_pipelined_rejections_are_exercised(warm):
+    """The re-run-after-rejection path of the pipelined loop, on its own: from
+    a converged triplet state (warm rounds; on this small instance twins keep
+    improving, triplets do not) keep-if-improved rounds get rejected, and the
+    pipelined loop still equals the serial one."""
+    mode, n = _lib.SH_MODE_TRIPLETS, 8
+    from cpu_engine import CPUOracleEngine
+    sd = D.synthetic(**SMALL)
+    start = torch.from_numpy(sd.types.copy())
+    run_rounds(CPUOracleEngine(sd.wish, sd.goodkids, sd.nq), start, mode=mode, n=n, seed=99,
+               max_rounds=warm, patience=100, world=World())
+    _, rejected = _serial_vs_pipelined(sd, start, mode, n, None, 100, 8)
+    assert rejected, "no round was rejected: the re-run path was not exercised"
 
 
 def test_triplet_rounds_keep_units():
@@ -197,3 +209,71 @@ def test_triplet_rounds_keep_units():
     assert_disjoint(rows, _lib.SH_MODE_TRIPLETS)
     with pytest.raises(AssertionError):  # units (c, c+1, c+2) and (c+2, ...) overlap
         assert_disjoint(torch.tensor([3, 5], dtype=torch.int32), _lib.SH_MODE_TRIPLETS)
+
+
+@pytest.mark.parametrize("pipeline,check", [(False, False), (True, False), (False, True), (True, True)])
+def test_device_error_flags_raise(pipeline, check):
+    """A block the device skipped (error flags set) is never accepted
+    silently: run_rounds raises at its end, and after the round itself with
+    --check-disjoint, in the serial and the pipelined loop."""
+    from cpu_engine import CPUOracleEngine
+    sd = D.synthetic(**SMALL)
+
+    class Flagged(CPUOracleEngine):
+        rounds_solved = 0
+
+        def solve_blocks(self, *a, **kw):
+            self.rounds_solved += 1
+            return super().solve_blocks(*a, **kw)
+
+        def error_flags(self):
+            return _lib.SH_ERRF_TYPE
+
+    eng = Flagged(sd.wish, sd.goodkids, sd.nq)
+    with pytest.raises(RuntimeError, match="error flags"):
+        run_rounds(eng, torch.from_numpy(sd.types.copy()), mode=0, n=64, seed=1, max_rounds=3,
+                   patience=100, world=World(), pipeline=pipeline, check_disjoint=check)
+    assert eng.rounds_solved == (1 if check else 3)
+
+
+@pytest.mark.parametrize("mode,n", [(0, 64), (1, 16), (2, 8)])
+@pytest.mark.parametrize("pipeline", [False, True])
+@pytest.mark.parametrize("every", [1, 3])
+def test_delta_sums_equal_full_rescore(mode, n, pipeline, every):
+    """SURVEY §8(e)'s delta all-reduce (each round's sums = the start state's
+    + the blocks' exact deltas; a full rescore every K rounds must agree)
+    gives the full-rescore loop's history, decisions and state, including
+    keep-if-improved rollbacks (from a converged state) and the pipelined loop."""
+    from cpu_engine import CPUOracleEngine
+    sd = D.synthetic(**SMALL)
+    start = torch.from_numpy(sd.types.copy())
+    run_rounds(CPUOracleEngine(sd.wish, sd.goodkids, sd.nq), start, mode=mode, n=n, seed=99,
+               max_rounds=12, patience=100, world=World())
+    out = []
+    for k in (0, every):
+        t = start.clone()
+        res = run_rounds(CPUOracleEngine(sd.wish, sd.goodkids, sd.nq), t, mode=mode, n=n, seed=5,
+                         max_rounds=7, patience=2, world=World(), pipeline=pipeline, score_check_every=k)
+        out.append((t.numpy().copy(), [(st.round, st.s_child, st.s_gift, st.score, st.accepted, st.best)
+                                       for st in res.history]))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_delta_mismatch_raises(pipeline):
+    """A delta that disagrees with the full rescore stops the run at the
+    first check round."""
+    from cpu_engine import CPUOracleEngine
+    sd = D.synthetic(**SMALL)
+
+    class Off(CPUOracleEngine):
+        def solve_blocks(self, mode, rows, n, types, delta=None):
+            super().solve_blocks(mode, rows, n, types, delta=delta)
+            if delta is not None:
+                delta[1] += 1
+
+    with pytest.raises(RuntimeError, match="full rescore"):
+        run_rounds(Off(sd.wish, sd.goodkids, sd.nq), torch.from_numpy(sd.types.copy()), mode=0, n=64,
+                   seed=1, max_rounds=5, patience=100, world=World(), pipeline=pipeline,
+                   score_check_every=2)

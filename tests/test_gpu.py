@@ -202,7 +202,8 @@ def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
     # register-tile design for the fallback launch, the LDS-tile kernel for its
     # windowed-key re-solve -- the path of an out-of-range block)
     if mode == 0 and n <= 256:
-        flag_sets = (0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1, _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_TEST_RANGE,
+        flag_sets = (0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_SP2, _lib.SH_FLAG_SP1,
+                     _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_TEST_RANGE,
                      _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_LDS_TILE | _lib.SH_FLAG_TEST_RANGE,
                      _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_VT_TILE | _lib.SH_FLAG_TEST_RANGE)
     elif mode == 1 and n <= 256:
@@ -257,6 +258,84 @@ def test_full_round_properties(sh, ctx, full_data):
     assert np.array_equal(c[pick], ocol)
     assert np.array_equal(cost.cpu().numpy()[pick], ocost)
     assert np.array_equal(t1[r[pick].reshape(-1)], t_host[r[pick].reshape(-1)])
+
+
+def _oracle_round_threaded(mode, wish, t_host, r, ng, threads=16):
+    """oracle.round_blocks over every block of a round, split over threads
+    (ctypes releases the GIL; the blocks are disjoint, so the threads apply
+    their swaps to the one host type vector without conflicts)."""
+    import concurrent.futures as cf
+    B = r.shape[0]
+    col = np.zeros(r.shape, dtype=np.int64)
+    cost = np.zeros(B, dtype=np.int64)
+    steps = np.zeros(B, dtype=np.uint64)
+    chunk = (B + threads - 1) // threads
+
+    def work(b0):
+        b1 = min(B, b0 + chunk)
+        st = np.zeros(2, dtype=np.uint64)
+        c, k = oracle.round_blocks(mode, wish, t_host, r[b0:b1], stats=st, ng=ng)
+        col[b0:b1], cost[b0:b1] = c, k
+        return int(st[0])
+
+    with cf.ThreadPoolExecutor(threads) as ex:
+        total_steps = sum(ex.map(work, range(0, B, chunk)))
+    return col, cost, total_steps
+
+
+@pytest.mark.parametrize("mode,pinned,rounds", [(0, (1, 10, 19), 20), (1, (0, 10), 11)])
+def test_bench_rounds_vs_oracle(sh, ctx, full_data, mode, pinned, rounds):
+    """The rounds bench.py times, pinned to the oracle on the states they
+    actually run from: bench seed 2017, full rounds (3730 singles blocks on the
+    default dispatch, santa_sp2_kernel; 78 twins blocks), the reference's loop
+    (run_rounds).  At the pinned rounds ALL blocks' col and exact cost, the
+    whole new type vector and the steps equal the oracle solving the same
+    pre-round state; every round's (S_child, S_gift) equals the oracle's
+    rescore (mpi_single.py:119-157, mpi_twins.py:121-169)."""
+    from santa_hip import _lib
+    from santa_hip.driver import GPUEngine, World, run_rounds
+    n = 256
+    _, _, _, nb = ctx.geometry(mode, n)
+    assert ctx.solve_design(mode, n, nb) == (_lib.SH_DESIGN_SPARSE3 if mode == 0 else _lib.SH_DESIGN_TWINS)
+    checked = []
+
+    class Pin(GPUEngine):
+        calls = 0
+
+        def solve_blocks(self, mode_, rows_, n_, types_, delta=None):
+            k = self.calls
+            self.calls += 1
+            if k not in pinned:
+                return super().solve_blocks(mode_, rows_, n_, types_, delta=delta)
+            B = rows_.numel() // n_
+            pre = types_.cpu().numpy()
+            col = torch.empty(B * n_, dtype=torch.int32, device="cuda")
+            cost = torch.empty(B, dtype=torch.int64, device="cuda")
+            steps = torch.empty(B, dtype=torch.int64, device="cuda")
+            delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+            self.ctx.solve_blocks(mode_, rows_, n_, types_, col=col, cost=cost, delta=delta, steps=steps)
+            t_host = pre.copy()
+            r = rows_.cpu().numpy().reshape(B, n_)
+            ocol, ocost, osteps = _oracle_round_threaded(mode_, full_data.wish, t_host, r, full_data.ng)
+            assert np.array_equal(col.cpu().numpy().reshape(B, n_), ocol), k
+            assert np.array_equal(cost.cpu().numpy(), ocost), k
+            assert np.array_equal(types_.cpu().numpy(), t_host), k
+            assert int(steps.sum()) == osteps, k
+            s0 = oracle.score_sums(full_data.wish, full_data.goodkids, pre)
+            s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
+            assert delta.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]], k
+            checked.append(k)
+
+        def score_sums(self, t):
+            s = super().score_sums(t)
+            assert s == oracle.score_sums(full_data.wish, full_data.goodkids, t.cpu().numpy())
+            return s
+
+    types = ctx.upload_types(full_data.types)
+    res = run_rounds(Pin(ctx), types, mode=mode, n=n, seed=2017, max_rounds=rounds, patience=1 << 30,
+                     world=World())
+    assert checked == list(pinned) and res.rounds == rounds
+    assert ctx.error_flags() == 0
 
 
 @pytest.mark.parametrize("mode,n", [(0, 2000), (1, 3000)])
@@ -470,6 +549,22 @@ def test_lsap_wide_range_int64_uses_exact_fallback(sh):
         sh.solve_batched(torch.from_numpy(C * 4).cuda())
 
 
+@pytest.mark.parametrize("maximize", [False, True])
+def test_lsap_int64_min_takes_float_path(sh, maximize):
+    """An int64 entry at INT64_MIN (np.abs and negation wrap there) is out of
+    the exact-int64 range: linear_sum_assignment replays scipy's float64
+    arithmetic instead, for minimise and maximise alike."""
+    rng = np.random.default_rng(3)
+    C = rng.integers(-50, 50, size=(9, 9), dtype=np.int64)
+    C[2, 5] = np.iinfo(np.int64).min
+    _, got = sh.linear_sum_assignment(C, maximize=maximize)
+    Cf = C.astype(np.float64)
+    _, want = oracle.lsap(-Cf if maximize else Cf)
+    assert np.array_equal(got, want)
+    with pytest.raises(ValueError):
+        sh.solve_batched(torch.from_numpy(C[None]).cuda())
+
+
 def test_no_fallback_on_santa_rounds(sh, ctx, full_data):
     """Santa cost spreads stay inside the packed key's window: the exact
     two-pass argmin is never needed on real rounds (performance guard)."""
@@ -492,7 +587,7 @@ def _round_outputs(ctx, full_data, mode, rows, nn, B, fl=0):
     return [x.cpu().numpy() for x in (col, cost, delta, steps, types)]
 
 
-@pytest.mark.parametrize("design", ["tile2", "sp1"])
+@pytest.mark.parametrize("design", ["tile2", "tile2_sp2", "sp1"])
 def test_sparse_overflow_fallback(sh, ctx, full_data, design):
     """Blocks that do not fit the sparse kernels' on-chip capacity (sp1: the
     LDS hit-list budget; tile2: the overflow list of rows with more than 32
@@ -504,8 +599,9 @@ def test_sparse_overflow_fallback(sh, ctx, full_data, design):
     B, nn = 96, 256
     rows = ctx.sample_blocks(0, nn, B, 5, 3)
     want = _round_outputs(ctx, full_data, 0, rows, nn, B, _lib.SH_FLAG_VT_TILE)
-    fl = _lib.SH_FLAG_SP_TILE if design == "tile2" else _lib.SH_FLAG_SP1
-    budgets = (16, 1600, 2400, 0, 0, 800, 0) if design == "tile2" else (6000, 16500, 17500, 0, 0, 4096, 0)
+    fl = {"tile2": _lib.SH_FLAG_SP_TILE, "tile2_sp2": _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_SP2,
+          "sp1": _lib.SH_FLAG_SP1}[design]
+    budgets = (16, 1600, 2400, 0, 0, 800, 0) if design != "sp1" else (6000, 16500, 17500, 0, 0, 4096, 0)
     try:
         for budget in budgets:
             cap = ctx.set_sparse_budget(budget)
@@ -520,16 +616,16 @@ def test_sparse_overflow_fallback(sh, ctx, full_data, design):
 
 def test_kernel_designs_agree(sh, ctx, full_data):
     """The one-wave sparse-tile kernel (SH_FLAG_SP_TILE), the default dispatch, the 4-wave
-    register-tile kernel (SH_FLAG_VT_TILE), the one-wave register kernel
-    (SH_FLAG_SW_TILE) and the 4-wave LDS-tile kernel (SH_FLAG_LDS_TILE)
-    produce identical rounds: col, cost, deltas, steps, state."""
+    register-tile kernel (SH_FLAG_VT_TILE) and the 4-wave LDS-tile kernel
+    (SH_FLAG_LDS_TILE) produce identical rounds: col, cost, deltas, steps,
+    state.  The retired one-wave register kernel's flag is refused."""
     from santa_hip import _lib
     mode = 0
     for B, nn in ((64, 256), (16, 100), (8, 37), (8, 130), (4, 1), (6, 255), (5, 64)):
         rows = ctx.sample_blocks(mode, nn, B, 77, 9)
         outs = []
-        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_SP1, _lib.SH_FLAG_VT_TILE,
-                   _lib.SH_FLAG_SW_TILE, _lib.SH_FLAG_LDS_TILE):
+        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_SP2, _lib.SH_FLAG_SP1,
+                   _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_LDS_TILE):
             types = ctx.upload_types(full_data.types)
             col = torch.empty(B * nn, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -541,6 +637,11 @@ def test_kernel_designs_agree(sh, ctx, full_data):
         for other in outs[1:]:
             for x, y in zip(outs[0], other):
                 assert np.array_equal(x, y), (B, nn)
+    types = ctx.upload_types(full_data.types)
+    with pytest.raises(ValueError, match="retired"):
+        ctx.solve_blocks(mode, ctx.sample_blocks(mode, 256, 4, 1, 0), 256, types, flags=_lib.SH_FLAG_SW_TILE)
+    with pytest.raises(ValueError, match="retired"):
+        ctx.solve_design(mode, 256, 4, _lib.SH_FLAG_SW_TILE)
 
 
 def test_shard_designs_agree(sh, ctx, full_data):
@@ -573,13 +674,14 @@ def test_design_dispatch(sh, ctx):
     fits in one resident wave of those (the shard at 4 GPUs: 933), the sparse
     kernel again when forced; twins and large blocks have one design each."""
     from santa_hip import _lib
-    assert ctx.solve_design(0, 256, 3730) == 6
+    assert ctx.solve_design(0, 256, 3730) == _lib.SH_DESIGN_SPARSE3
+    assert ctx.solve_design(0, 256, 3730, _lib.SH_FLAG_SP2) == _lib.SH_DESIGN_SPARSE2
     assert ctx.solve_design(0, 256, 466) == 1
-    assert ctx.solve_design(0, 256, 466, _lib.SH_FLAG_SP_TILE) == 6
+    assert ctx.solve_design(0, 256, 466, _lib.SH_FLAG_SP_TILE) == _lib.SH_DESIGN_SPARSE3
     assert ctx.solve_design(0, 256, 3730, _lib.SH_FLAG_SP1) == 0
     assert ctx.solve_design(0, 256, 933) == 3
     assert ctx.resident_blocks(0, 256, 933) >= 933
-    assert ctx.solve_design(0, 256, 1865) == 6
+    assert ctx.solve_design(0, 256, 1865) == _lib.SH_DESIGN_SPARSE3
     # the register-tile design holds a whole round at once (4 waves per SIMD)
     assert ctx.resident_blocks(0, 256, 3730) >= 3730
     assert ctx.solve_design(1, 256, 78) == 4
@@ -678,7 +780,8 @@ def test_santa_edge_block_sizes_vs_oracle(sh, ctx, full_data, mode, n, B):
                                       ng=full_data.ng)
     s0 = oracle.score_sums(full_data.wish, full_data.goodkids, full_data.types)
     s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
-    for fl in ((0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1) if mode == 0 else (0,)):
+    for fl in ((0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_SP2, _lib.SH_FLAG_SP1)
+               if mode == 0 else (0,)):
         types = ctx.upload_types(full_data.types)
         col = torch.empty(B * n, dtype=torch.int32, device="cuda")
         cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -723,16 +826,21 @@ def test_two_ranks_on_the_hip_path_equal_one_rank(sh, ctx, full_data, mode, roun
     out = mgr.dict()
     mp.spawn(rank_main, args=(2, port, mode, 256, rounds, 41, out), nprocs=2, join=True)
     for r in range(2):
-        t, sm, scores, flags = out[r]
+        t, sm, scores, flags, full = out[r]
         assert flags == 0
         assert np.array_equal(t, want), f"rank {r} state differs"
-        assert sm == sums, f"rank {r} per-round sums differ"
+        # two ranks take each round's sums from the delta all-reduce (§8(e));
+        # they equal the one-rank run's full rescore of every round
+        assert sm == sums[1:], f"rank {r} per-round sums differ"  # (sums[0]: the start state)
         assert scores == [st.score for st in res.history]
+        assert full == sums[:1]  # one rescore (the start state); the last round's check is internal
 
 
 def test_bench_launches_n_ranks(sh):
     """`bench.py --gpus 2` started by hand launches its two ranks itself and
-    reports n_gpus = 2 (here both on the one GPU of the box, over gloo)."""
+    reports n_gpus = 2 (here both on the one GPU of the box, over gloo), with
+    the CPU baselines (timed by the launcher before the ranks start: the
+    reference's round B1 and the C port) on the N > 1 line too."""
     import json
     import os
     import subprocess
@@ -740,16 +848,20 @@ def test_bench_launches_n_ranks(sh):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2",
-                        "--warmup", "1", "--one-device", "--dist-backend", "gloo", "--no-cpu-baseline"],
+                        "--warmup", "1", "--one-device", "--dist-backend", "gloo", "--cpu-seconds", "1",
+                        "--b1-seconds", "1"],
                        capture_output=True, text=True, timeout=240, env=env, cwd=root)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert line["config"]["blocks_per_round"] == 3730
+    cb = line["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    assert set(cb["b1_blocks_per_s"]) and all(v > 0 for v in cb["b1_blocks_per_s"].values())
 
 
 # --------------------------------------------------------------------------- input validation
-@pytest.mark.parametrize("mode,n,fl", [(0, 256, 128), (0, 256, 256), (0, 256, 8), (0, 256, 32), (0, 256, 16),
+@pytest.mark.parametrize("mode,n,fl", [(0, 256, 128), (0, 256, 256), (0, 256, 8), (0, 256, 32),
                                        (1, 256, 0), (0, 300, 0), (1, 300, 0)])
 def test_gift_type_out_of_range_is_flagged_not_used(sh, ctx, full_data, mode, n, fl):
     """A current gift type outside [0, ng) in a block (it would index the
@@ -850,8 +962,8 @@ def test_no_apply_solves_overlapping_blocks(sh, ctx, full_data):
         C = oracle.cost_single(full_data.wish, full_data.types, r[b], ng=full_data.ng)
         _, oc = oracle.lsap(C)
         want.append((oc, int(C[np.arange(n), oc].sum())))
-    for fl in (0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1, _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_VT_TILE,
-               _lib.SH_FLAG_SW_TILE):
+    for fl in (0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_SP2, _lib.SH_FLAG_SP1,
+               _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_VT_TILE):
         types = ctx.upload_types(full_data.types)
         col = torch.empty(B * n, dtype=torch.int32, device="cuda")
         cost = torch.empty(B, dtype=torch.int64, device="cuda")

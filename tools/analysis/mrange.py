@@ -1,0 +1,53 @@
+"""Analysis (not product code): the miss-count component m of the SAP's
+values on Santa singles blocks over the rounds the bench runs (seed 2017,
+full 3730-block rounds of n=256), see mrange.c.  Prints per sampled round the
+largest |m| of u, v, r/spc and minVal over the sampled blocks."""
+import concurrent.futures as cf
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "mpi-hungarian-method_amd"), os.path.join(ROOT, "oracle")]
+import oracle  # noqa: E402
+from santa_hip import data as D  # noqa: E402
+from santa_hip.sampler import sample_blocks, single_geometry  # noqa: E402
+
+so = "/tmp/libmrange.so"
+subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(os.path.dirname(__file__), "mrange.c")],
+               check=True)
+L = ctypes.CDLL(so)
+L.mrange_block.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+per = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+sd = D.synthetic(2017)
+tri, tw = sd.families
+lo, count, nb = single_geometry(sd.nc, n, tri, tw)
+t = sd.types.copy()
+worst = np.zeros(4, dtype=np.int32)
+for rnd in range(rounds):
+    rows = sample_blocks(2017, rnd, lo, count, 1, n, nb)
+    pick = np.random.default_rng(rnd).choice(nb, min(per, nb), replace=False)
+    mx = np.zeros(4, dtype=np.int32)
+    bad = 0
+
+    def one(b):
+        C = oracle.cost_single(sd.wish, t, rows[b], ng=sd.ng)
+        out = np.zeros(4, dtype=np.int32)
+        nb_ = L.mrange_block(n, C.ctypes.data, out.ctypes.data)
+        return out, nb_
+
+    with cf.ThreadPoolExecutor(8) as ex:
+        for out, b_ in ex.map(one, pick):
+            mx = np.maximum(mx, out)
+            bad += b_
+    worst = np.maximum(worst, mx)
+    print(f"round {rnd}: max|m| u {mx[0]} v {mx[1]} r {mx[2]} minVal {mx[3]}  undecodable {bad}", flush=True)
+    chunks = [rows[i:i + 64] for i in range(0, nb, 64)]
+    with cf.ThreadPoolExecutor(8) as ex:
+        list(ex.map(lambda ch: oracle.round_blocks(0, sd.wish, t, ch, ng=sd.ng), chunks))
+print("worst", worst.tolist())
