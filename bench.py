@@ -32,6 +32,17 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-hungarian-method_amd"))
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# LDS: 256 CUs x 256 B/clk (ds_read_b64/b128 rate per CU, MI355X_MICROARCH.md
+# LDS table) x 2.4 GHz
+LDS_PEAK_TBS = 256 * 256 * 2.4e9 / 1e12
+# Algorithmic LDS bytes of the solve per Dijkstra step and per Dijkstra (all
+# lanes of the block's waves): santa_sp3_kernel per step =
+# 64 lanes x (4 scatter + 16 row read + 4 un-scatter + 4 u + 1 + 1 remaining),
+# per Dijkstra 64 x (4 remaining + 16 dual atomics); santa_sp2_kernel the
+# same with 8-byte costs and duals; the 4-wave kernels per step = 256 threads
+# x (1 tile byte + 4 u + 8 step word) + the fold, per Dijkstra 256 x 12.
+LDS_BYTES = {"santa_sp3_kernel": (64 * 30, 64 * 20), "santa_sp2_kernel": (64 * 58, 64 * 36),
+             "santa_block_kernel": (256 * 13, 256 * 12), "santa_vt_kernel": (256 * 12, 256 * 12)}
 CLOCK_HZ = 2.4e9               # MI355X max shader clock (MI355X_MICROARCH.md)
 KERNEL_SRC = os.path.join(ROOT, "mpi-hungarian-method_amd", "csrc", "santa_hip.hip")
 
@@ -279,6 +290,23 @@ def design_kernels(kname: str):
     return ["santa_tile_kernel", k] if k in ("santa_sp2_kernel", "santa_sp3_kernel") else [k]
 
 
+def stored_occupancy(kname: str):
+    """Mean resident waves per SIMD and LDS-array activity of `kname` from
+    the newest committed PMC summary of THIS kernel source (the "occ" pass of
+    tools/profile_round.sh, round-0 launch), or None."""
+    src = hashlib.sha256(open(KERNEL_SRC, "rb").read()).hexdigest()[:16]
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
+        try:
+            s = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if s.get("source_sha16") == src and kname in s.get("occupancy_lds", {}):
+            e = dict(s["occupancy_lds"][kname])
+            e["source"] = f"{os.path.basename(path)} (round-0 launch, kernel source {src})"
+            return e
+    return None
+
+
 def stored_traffic(knames):
     """HBM bytes per launch of the kernels `knames` (summed) from the newest committed rocprofv3 PMC
     summary taken on THIS kernel source (tools/profile_round.sh ->
@@ -446,6 +474,7 @@ def main():
     # per-step latency is measured by re-running round 0's longest block
     # alone (same kernel design, untimed region).
     latency = None
+    lds = None
     if my_blocks:
         st = steps_dev[:min(launches, max_calls), :my_blocks].cpu().numpy().astype(np.int64)
         bmax = int(st[0].argmax())
@@ -470,6 +499,18 @@ def main():
         occ_floor = float(st.sum()) * s_per_step / max(min(resident, my_blocks), 1)
         kern_sum = float(np.sum(kern_ms)) / 1e3
         floor = max(chain_floor, occ_floor)
+        kshort = kname.split(" ")[0]
+        lds = None
+        if kshort in LDS_BYTES:
+            per_step, per_dij = LDS_BYTES[kshort]
+            lds_b = float(st.sum()) * per_step + my_blocks * n * per_dij * len(st)
+            ach = lds_b / kern_sum / 1e12 if kern_sum > 0 else 0.0
+            lds = {"bound": "lds", "achieved": round(ach, 3), "peak": round(LDS_PEAK_TBS, 1), "unit": "TB/s",
+                   "frac": round(ach / LDS_PEAK_TBS, 4), "bytes_per_step": per_step, "bytes_per_dijkstra": per_dij,
+                   "note": "algorithmic LDS bytes of the solve (steps of the timed launches) / kernel time"}
+            occ = stored_occupancy(kshort)
+            if occ:
+                lds["pmc"] = occ
         latency = {"steps_per_launch": float(st.sum(axis=1).mean()),
                    "steps_max_block_per_launch": float(st.max(axis=1).mean()),
                    "round0_steps": int(st[0].sum()), "round0_max_block_steps": int(st[0].max()),
@@ -519,7 +560,7 @@ def main():
                                  "per block / kernel time); the kernel is bound by its serial "
                                  "Dijkstra chains, see latency",
                      "kernel": kname, "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
-                     "algorithmic_bytes_per_block": per_block, "latency": latency},
+                     "algorithmic_bytes_per_block": per_block, "latency": latency, "lds": lds},
         "cpu": cpu,
     }
     if world == 1:  # the PMC passes profile a full one-GPU round (tools/profile_round.sh)

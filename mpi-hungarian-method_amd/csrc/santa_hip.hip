@@ -696,6 +696,152 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
   return __syncthreads_or(big) != 0;
 }
 
+// Lattice units of santa_sp3_kernel and sap_solve_mw_l32 (see santa_sp3_kernel).
+constexpr int SP3_SH = 11;                  // key tie-break field: class 1 | pkey 8 | k 2
+constexpr int32_t SP3_BIAS = 1 << 20;       // spc_V + BIAS in [0, 2^21) (key field)
+constexpr uint32_t SP3_INF = (1u << 21) - 1u;  // "infinite" spc (never a live winner)
+
+// V = A * 512 + m with |A| <= amax and |m| <= mmax (2 * mmax < 512)
+__device__ __forceinline__ bool sp3_in_range(int32_t V, int amax, int mmax) {
+  return (((uint32_t)(V + mmax) & 511u) <= (uint32_t)(2 * mmax)) &&
+         ((uint32_t)(V + amax * 512 + mmax) <= (uint32_t)(2 * (amax * 512 + mmax)));
+}
+
+// ---------------------------------------------------------------------------
+// sap_solve_mw_l32: sap_solve_mw_sc's decisions in santa_sp3_kernel's 32-bit
+// lattice units (singles, n <= 256, one column per thread, NW waves): a wish
+// costs -a * 512, a miss 1 (V = A * 512 + m, exact while the checked range
+// holds, see santa_sp3_kernel), key = (spc_V + 2^20) << 11 | class << 10 |
+// pkey << 2.  The step word is 64-bit: (0xFFFF - step) << 48 | key << 16 |
+// aux (aux = assigned ? row : column); a step's words are below every older
+// one, so one word serves every step with no re-arm (a block takes at most
+// n (n + 1) / 2 <= 32,896 steps).  Returns true (block-wide) when the range
+// was left: the caller re-solves with sap_solve_mw.  u lives in S.u as int32.
+// ---------------------------------------------------------------------------
+// TIMED (dev): shader cycles of wave 0 per segment, summed over the solve, in
+// seg[0..3]: A = row and dual loads up to the relaxation's inputs; B =
+// relaxation, row argmin and the fold into the step word; C = the barrier,
+// the word's read and decode; D = per-Dijkstra set-up, dual update, augment.
+template <int NW, bool TIMED = false, typename Loader, typename... LA>
+__device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, const SolveLds &S,
+                                                 int64_t &steps_out, bool big, int64_t E, uint64_t *seg,
+                                                 const LA &...la) {
+  const int tid = threadIdx.x, j = tid;
+  const bool colv = j < n;
+  int32_t *u32 = (int32_t *)S.u;
+  const int Mm = (int)min((int64_t)199, (int64_t)(0xFFFFFFFFll / E) / 2);
+  const int mW = (Mm - 1) / 3, mU = Mm - 1 - mW;
+  uint32_t sb = SP3_INF;
+  int32_t W = 0;  // -v (this thread's column)
+  int path = -1, pos = -1, r4c = -1;
+  uint32_t lo = 0, aux = 0;
+  uint32_t accm = 0, acca = 0;
+  int steps = 0;
+  uint64_t tA = 0, tB = 0, tC = 0, tD = 0, ts = 0;
+  auto stamp = [&](uint64_t &acc) {
+    if constexpr (TIMED) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      acc += t - ts;
+      ts = t;
+    }
+  };
+  if constexpr (TIMED) ts = __builtin_amdgcn_s_memtime();
+  for (int r = tid; r < n; r += NW * WAVE) u32[r] = 0;
+  if (tid == 0) S.red[0] = ~0ull;
+  __syncthreads();
+  for (int cur = 0; cur < n; ++cur) {
+    sb = SP3_INF;
+    pos = colv ? (n - 1 - j) : -1;
+    r4c = colv ? S.r4c[j] : -1;
+    lo = (r4c < 0) ? ((255u - (uint32_t)pos) << 2) : (((1u << 8) | (uint32_t)pos) << 2);
+    aux = (r4c < 0) ? (uint32_t)j : (uint32_t)r4c;
+    int nrem = n;
+    int32_t minVal = 0;
+    int i = cur;
+    int sink;
+    bool first = true;
+    for (;;) {
+      ++steps;
+      stamp(first ? tD : tC);
+      first = false;
+      const int32_t uraw = u32[i];
+      int32_t c;
+      ld.load(i, c, la...);
+      const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
+      if constexpr (TIMED) {
+        asm volatile("" ::"v"(c), "s"(ui));
+        stamp(tA);
+      }
+      accm = max(accm, (uint32_t)(ui + mU) & 511u);
+      acca = max(acca, (uint32_t)(ui < 0 ? -ui : ui));
+      const uint32_t bse = (uint32_t)(SP3_BIAS - ui);
+      const bool act = pos >= 0;
+      const uint32_t r = (uint32_t)W + (uint32_t)c + bse;
+      const bool upd = act && (r < sb);
+      sb = upd ? r : sb;
+      path = upd ? i : path;
+      const uint32_t key = act ? ((sb << SP3_SH) | lo) : ~0u;
+      // row minimum (every lane holds its 16-lane row's), its holders fold
+      // (tag, key, aux) into the step word
+      const uint32_t mh = row_min_u32_dpp(key);
+      if (key == mh && mh != ~0u)
+        __hip_atomic_fetch_min(S.red, ((uint64_t)(0xFFFFu - (uint32_t)steps) << 48) | ((uint64_t)key << 16) | aux,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      stamp(tB);
+      __syncthreads();
+      const uint64_t g = S.red[0];
+      const uint32_t gk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 16));
+      const int ga = __builtin_amdgcn_readfirstlane((int)(uint32_t)g) & 0xFF;
+      minVal = (int32_t)(gk >> SP3_SH) - SP3_BIAS;
+      const bool assigned = (gk >> 10) & 1u;
+      const int pk = (int)((gk >> 2) & 255u);
+      const int pstar = assigned ? pk : 255 - pk;
+      const int last = nrem - 1;
+      lo ^= (pos == last) ? ((uint32_t)(last ^ pstar) << 2) : 0u;  // the mover's position key
+      pos = (pos == pstar) ? -1 : ((pos == last) ? pstar : pos);
+      --nrem;
+      if (!assigned) {
+        sink = ga;
+        break;
+      }
+      i = ga;
+    }
+    // dual update and path dump (sap_solve_mw_sc's, in V units)
+    if (colv && pos < 0) {
+      const int32_t d = (int32_t)((uint32_t)(minVal + SP3_BIAS) - sb);
+      W += d;
+      if (r4c >= 0) u32[r4c] += d;
+      S.path[j] = (int16_t)path;
+    }
+    big |= !sp3_in_range(W, 500, mW);
+    if (tid == 0) u32[cur] += minVal;
+    __syncthreads();
+    if (tid == 0) {  // augment along the path from the sink back to cur
+      int jj = sink;
+      for (;;) {
+        const int pi = S.path[jj];
+        S.r4c[jj] = (int16_t)pi;
+        const int t = S.c4r[pi];
+        S.c4r[pi] = (int16_t)jj;
+        jj = t;
+        if (pi == cur) break;
+      }
+    }
+    __syncthreads();
+  }
+  stamp(tD);
+  if constexpr (TIMED) {
+    seg[0] = tA;
+    seg[1] = tB;
+    seg[2] = tC;
+    seg[3] = tD;
+  }
+  big |= accm > (uint32_t)(2 * mU) || acca > (uint32_t)(1000 * 512 + mU);
+  if (colv) big |= !sp3_in_range(u32[j], 1000, mU);
+  steps_out = steps;
+  return __syncthreads_or(big) != 0;
+}
+
 // ---------------------------------------------------------------------------
 // Row loaders: return row i's costs of this thread's K columns.
 // ---------------------------------------------------------------------------
@@ -709,6 +855,15 @@ struct TileU8Loader {  // singles: uint8 rank codes, row stride RS bytes (costs 
     const uint8_t *p = tile + (size_t)i * RS + w * (WAVE * K) + lane;
 #pragma unroll
     for (int k = 0; k < K; ++k) c[k] = (int64_t)((uint64_t)single_cost(p[k * WAVE], nw1, E) << SH);
+  }
+};
+
+struct TileU8LoaderV {  // singles: uint8 rank codes -> lattice V (a wish -a * 512, a miss 1)
+  const uint8_t *tile;
+  int RS, nw1;
+  __device__ __forceinline__ void load(int i, int32_t &c) const {
+    const uint32_t code = tile[(size_t)i * RS + threadIdx.x];
+    c = code ? (int32_t)((code - (uint32_t)nw1) << 9) : 1;
   }
 };
 
@@ -854,7 +1009,7 @@ __host__ __device__ __forceinline__ SantaLds santa_lds_layout(int n, int mode, i
   return L;
 }
 
-template <int K, int MODE>
+template <int K, int MODE, bool TIMED = false>
 __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   static_assert(K == 1, "one column per thread (n <= 256)");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -988,6 +1143,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   // -- solve ------------------------------------------------------------------
   int64_t steps = 0;
   int fallbacks = 0;
+  uint64_t seg[4] = {0, 0, 0, 0};  // (TIMED: sap_solve_mw_l32's segments)
   const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
   if (a.flags & SH_FLAG_BUILD_ONLY) {  // phase timing: tile build + apply identity
     for (int i = tid; i < n; i += SANTA_WG) S.c4r[i] = (int16_t)i;
@@ -1001,8 +1157,13 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
     if (!exact) {
       const bool force = (a.flags & SH_FLAG_TEST_RANGE) != 0;
       if constexpr (MODE == 0) {
-        const TileU8Loader<SANTA_NW, 1, SC_SH> ld{tile8, RS, nw1, a.E};
-        redo = sap_solve_mw_sc<SANTA_NW>(n, ld, S, steps, force);
+        if (a.flags & SH_FLAG_SP2) {  // (A/B: round 2's 64-bit scaled keys)
+          const TileU8Loader<SANTA_NW, 1, SC_SH> ld{tile8, RS, nw1, a.E};
+          redo = sap_solve_mw_sc<SANTA_NW>(n, ld, S, steps, force);
+        } else {
+          const TileU8LoaderV ld{tile8, RS, nw1};
+          redo = sap_solve_mw_l32<SANTA_NW, TIMED>(n, ld, S, steps, force, a.E, seg);
+        }
       } else {
         const TileU16Loader<SANTA_NW, 1, SC_SH> ld{(const uint16_t *)tile8, lut, RS};
         redo = sap_solve_mw_sc<SANTA_NW>(n, ld, S, steps, force);
@@ -1028,7 +1189,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   int64_t cost = 0, dch = 0, dgh = 0;
   for (int i = tid; i < n; i += SANTA_WG) {
     const int col = S.c4r[i];
-    if (a.col) a.col[(size_t)b * n + i] = col;
+    if (a.col && !TIMED) a.col[(size_t)b * n + i] = col;
     const int told = ctype[i], tnew = ctype[col];
     const int child = rows_l[i];
     if (MODE == 0) {
@@ -1080,6 +1241,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
       atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)td1);
     }
     if (fallbacks) atomicAdd(a.err + 1, fallbacks);
+    if (TIMED && a.col && n >= 4)  // (wave 0's segment cycles, see sap_solve_mw_l32)
+      for (int q = 0; q < 4; ++q) a.col[(size_t)b * n + q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
   }
 }
 
@@ -1194,6 +1357,18 @@ struct VtRegLoader {
     asm volatile("" : "+v"(w1));
     const uint32_t code = (((d < 32) ? w0 : w1) >> (8 * (i & 3))) & 0xFFu;
     c[0] = (int64_t)((uint64_t)single_cost(code, nw1, E) << SH);
+  }
+};
+
+struct VtRegLoaderV {  // VtRegLoader's code -> lattice V (santa_sp3_kernel's units)
+  int nw1;
+  __device__ __forceinline__ void load(int i, int32_t &c, const u32x32 &ta, const u32x32 &tb) const {
+    const int d = i >> 2;
+    uint32_t w0 = ta[d & 31], w1 = tb[d & 31];
+    asm volatile("" : "+v"(w0));
+    asm volatile("" : "+v"(w1));
+    const uint32_t code = (((d < 32) ? w0 : w1) >> (8 * (i & 3))) & 0xFFu;
+    c = code ? (int32_t)((code - (uint32_t)nw1) << 9) : 1;
   }
 };
 
@@ -1379,8 +1554,14 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
   } else if constexpr (SC) {
     bool redo = exact;
     if (!exact) {
-      const VtRegLoader<SC_SH> ld{nw1, a.E};
-      redo = sap_solve_mw_sc<VT_NW>(n, ld, S, steps, (a.flags & SH_FLAG_TEST_RANGE) != 0, T.a, T.b);
+      if (a.flags & SH_FLAG_SP2) {  // (A/B: round 2's 64-bit scaled keys)
+        const VtRegLoader<SC_SH> ld{nw1, a.E};
+        redo = sap_solve_mw_sc<VT_NW>(n, ld, S, steps, (a.flags & SH_FLAG_TEST_RANGE) != 0, T.a, T.b);
+      } else {
+        const VtRegLoaderV ld{nw1};
+        redo = sap_solve_mw_l32<VT_NW>(n, ld, S, steps, (a.flags & SH_FLAG_TEST_RANGE) != 0, a.E, nullptr,
+                                       T.a, T.b);
+      }
     }
     if (redo) {  // (block-uniform) left untouched for the windowed-key launch
       if (tid == 0) {
@@ -2760,49 +2941,26 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
 // tools/analysis/mrange.py; forced in the tests by SH_FLAG_TEST_RANGE).
 // Per step: ~50 VALU (santa_sp2_kernel: 108), no 64-bit LDS traffic.
 // ---------------------------------------------------------------------------
-constexpr int SP3_SH = 11;                  // key tie-break field: class 1 | pkey 8 | k 2
-constexpr int32_t SP3_BIAS = 1 << 20;       // spc_V + BIAS in [0, 2^21) (key field)
-constexpr uint32_t SP3_INF = (1u << 21) - 1u;  // "infinite" spc (never a live winner)
-
-// V = A * 512 + m with |A| <= amax and |m| <= mmax (2 * mmax < 512)
-__device__ __forceinline__ bool sp3_in_range(int32_t V, int amax, int mmax) {
-  return (((uint32_t)(V + mmax) & 511u) <= (uint32_t)(2 * mmax)) &&
-         ((uint32_t)(V + amax * 512 + mmax) <= (uint32_t)(2 * (amax * 512 + mmax)));
-}
-
-struct Sp3Lds {
-  size_t ctype, own, ovfr, ovf, u, rem, rowc, total;
-};
-
-__host__ __device__ __forceinline__ Sp3Lds sp3_lds_layout() {
-  Sp3Lds L;
-  size_t o = 0;
-  L.ctype = o;  o += 256 * 2;                  // column gift types (old)
-  L.own = o;    o += 256;                      // code(i, i): row i's own (old) gift
-  L.ovfr = o;   o += 256 * 4;                  // overflow range per row
-  L.ovf = o;    o += (size_t)SP2_OVF_CAP * 2;  // overflow entries
-  L.u = o;      o += (256 + 64) * 4;           // row duals V (+ a dump slot per lane)
-  L.rem = o;    o += 256;                      // scipy's `remaining`: column at position p
-  L.rowc = o;   o += (256 + 32) * 4;           // current row: C_V per column slot + dump slots
-  L.total = o;
-  return L;
-}
-
+// TIMED (SH_FLAG_TIMING, dev): shader-clock cycles per segment of the solve,
+// summed over the block, in col[b * n + 0..3]: A = a step's row fetch, scatter
+// and LDS reads up to the relaxation's inputs; B = relaxation, key and argmin;
+// C = winner decode and book-keeping; D = per-Dijkstra set-up, dual update and
+// augmentation.  (s_memtime stamps cost cycles themselves: relative view.)
+template <bool TIMED>
 __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const unsigned char *rec_all) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // (static LDS: every address below is a constant offset, no base register)
+  __shared__ __attribute__((aligned(16))) int32_t rowc[256 + 32];  // current row C_V per slot + dumps
+  __shared__ __attribute__((aligned(16))) int32_t u_l[256 + 64];   // row duals V + a dump slot per lane
+  __shared__ __attribute__((aligned(16))) uint32_t ovfr[256];      // overflow range per row
+  __shared__ __attribute__((aligned(16))) uint16_t ovf[SP2_OVF_CAP];  // overflow entries
+  __shared__ __attribute__((aligned(16))) int16_t ctype[256];     // column gift types (old)
+  __shared__ __attribute__((aligned(16))) uint8_t own[256];       // code(i, i): row i's own gift
+  __shared__ __attribute__((aligned(16))) uint8_t rem[256];       // scipy's `remaining`
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = a.n;
   const unsigned char *rec = rec_all + (size_t)b * SP2_REC;
   if (*(const volatile int32_t *)(rec + SP2_REC_STATUS)) return;  // skipped / left to the fallback
-  const Sp3Lds L = sp3_lds_layout();
-  int16_t *ctype = (int16_t *)(smem + L.ctype);
-  uint8_t *own = smem + L.own;
-  uint32_t *ovfr = (uint32_t *)(smem + L.ovfr);
-  uint16_t *ovf = (uint16_t *)(smem + L.ovf);
-  int32_t *u_l = (int32_t *)(smem + L.u);
-  uint8_t *rem = smem + L.rem;
-  int32_t *rowc = (int32_t *)(smem + L.rowc);
   const int x31 = lane & 31;
 
   // -- the tile into VGPRs (santa_sp2_kernel's record), the rest to LDS -------------
@@ -2838,7 +2996,15 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   const int mW = (Mm - 1) / 3, mU = Mm - 1 - mW;  // |m(W)| + |m(u~)| + 1 <= M
   __syncthreads();
   __builtin_amdgcn_s_setprio(3);  // (lowered over the last Dijkstras, below)
-  const uint64_t m1 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t tA = 0, tB = 0, tC = 0, tD = 0, ts = 0;
+  auto stamp = [&](uint64_t &acc) {
+    if constexpr (TIMED) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      acc += t - ts;
+      ts = t;
+    }
+  };
+  if constexpr (TIMED) ts = __builtin_amdgcn_s_memtime();
 
   uint32_t sb[4];      // spc_V + BIAS (columns 4*lane + k)
   int32_t W[4];        // -v_V
@@ -2890,14 +3056,18 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       uint32_t pglo = ~0u;
       int mv = -1;
       uint32_t kX = 0;
+      bool first = true;
       for (;;) {
         ++steps;
+        stamp(first ? tD : tC);
+        first = false;
         const uint32_t tw = tile2_get(T0, T1, i >> 2);
         const int32_t uraw = u_l[i];
         const int mover_v = rem[nrem - 1];  // the column at the last position
         const uint32_t e = (tw >> ((i & 1) << 4)) & 0xFFFFu;
-        const uint64_t hmask = ((i >> 1) & 1) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
-        const bool mine = __builtin_amdgcn_inverse_ballot_w64(hmask);
+        // the row's half of the wave (lanes 32L.., L = (i >> 1) & 1) as an SGPR mask
+        const uint32_t hl = (uint32_t)(-((i >> 1) & 1));
+        const bool mine = __builtin_amdgcn_inverse_ballot_w64(((uint64_t)hl << 32) | ~hl);
         const uint32_t ea = e >> 9;
         // book-keeping: the winner first (its tie bits are unique while it is
         // live; the mover's new bits may equal them), then the mover (a no-op
@@ -2907,26 +3077,29 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           lo[k] = (lo[k] == pglo) ? ~0u : lo[k];
           lo[k] ^= (l4 + k == mv) ? kX : 0u;
         }
-        // expand the row: hit columns get -a * 512, the rest hold a miss (1)
+        // expand the row: hit columns get -a * 512, the rest hold a miss (1);
+        // read this lane's four columns; put the misses back (in-order LDS)
         const int sslot = mine ? (int)(e & 0x1FFu) : 256 + x31;
         rowc[sslot] = -(int32_t)(ea << 9);
-        // (a row with more than 32 hits: the marker in its entry 31)
-        const bool ovr = __builtin_amdgcn_ballot_w64(mine && ea == SP2_MARK) != 0;
-        if (__builtin_expect(ovr, 0)) {
+        int2 c01, c23;
+        // (a row with more than 32 hits has the marker in its entry 31: one
+        // test for the whole slow path; the other half's marker only sends a
+        // row without overflow through it, count 0)
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(ea == SP2_MARK) != 0, 0)) {
           const uint32_t rg = ovfr[i];
           const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
           for (int x = lane; x < oc; x += WAVE) {
             const uint32_t e2 = ovf[os + x];
             rowc[e2 & 0x1FFu] = -(int32_t)((e2 >> 9) << 9);
           }
-        }
-        const int2 c01 = *(const int2 *)(rowc + 2 * lane);
-        const int2 c23 = *(const int2 *)(rowc + 128 + 2 * lane);
-        rowc[sslot] = 1;  // un-scatter (in-order LDS: after the reads)
-        if (__builtin_expect(ovr, 0)) {
-          const uint32_t rg = ovfr[i];
-          const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
+          c01 = *(const int2 *)(rowc + 2 * lane);
+          c23 = *(const int2 *)(rowc + 128 + 2 * lane);
+          rowc[sslot] = 1;
           for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = 1;
+        } else {
+          c01 = *(const int2 *)(rowc + 2 * lane);
+          c23 = *(const int2 *)(rowc + 128 + 2 * lane);
+          rowc[sslot] = 1;
         }
         const int32_t cc[4] = {c01.x, c01.y, c23.x, c23.y};
         // u~[i] = u[i] - minVal (row i is reached at the current minimum)
@@ -2934,7 +3107,12 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         // range of u~ (scalar): the largest m + mU field and the largest |V|
         accm = max(accm, (uint32_t)(ui + mU) & 511u);
         acca = max(acca, (uint32_t)(ui < 0 ? -ui : ui));
-        const uint32_t bse = (uint32_t)(SP3_BIAS - ui);
+        if constexpr (TIMED) {
+          asm volatile("" ::"v"(cc[0]), "v"(cc[3]), "s"(ui));
+          stamp(tA);
+        }
+        uint32_t bse = (uint32_t)(SP3_BIAS - ui);
+        asm volatile("" : "+s"(bse));  // (W + c + bse: one add3 per column)
         uint32_t best = ~0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -2947,6 +3125,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           best = key < best ? key : best;
         }
         const uint32_t g = wave_min_u32_dpp(best);
+        if constexpr (TIMED) {
+          asm volatile("" ::"s"(g));
+          stamp(tB);
+        }
         minVal = (int32_t)(g >> SP3_SH) - SP3_BIAS;
         const int kw = (int)(g & 3u);
         const uint32_t pkey = (g >> 2) & 255u;
@@ -3006,6 +3188,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       }
     }
   }
+  stamp(tD);
   __syncthreads();
 
   {  // the lattice range (see above): leave the block to the fallback launch
@@ -3021,7 +3204,6 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       return;
     }
   }
-  const uint64_t m2 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
   // -- outputs: lane handles rows i = 4*lane + k ------------------------------------
   int64_t cost = 0, dch = 0, dgh = 0;
 #pragma unroll
@@ -3050,7 +3232,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         dch += child_happy(cn, nw1) - child_happy(co, nw1);
         if (a.delta) dgh += gift_happy(a, chd, tnew) - gift_happy(a, chd, told);
       }
-      if (a.col) a.col[(size_t)b * n + i] = col;
+      if (a.col && !TIMED) a.col[(size_t)b * n + i] = col;
       if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[chd] = (int16_t)tnew;  // this block owns chd
     }
   }
@@ -3060,8 +3242,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   if (lane == 0) {
     if (a.cost) a.cost[b] = cost;
     if (a.steps) a.steps[b] = steps;
-    if ((a.flags & SH_FLAG_TIMING) && a.col && n > 1)  // solve, shader cycles
-      a.col[(size_t)b * n + 1] = (int32_t)min(m2 - m1, (uint64_t)INT32_MAX);
+    if (TIMED && a.col && n >= 4) {
+      const uint64_t seg[4] = {tA, tB, tC, tD};
+      for (int q = 0; q < 4; ++q) a.col[(size_t)b * n + q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
+    }
     if (a.delta) {
       atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
       atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
@@ -3784,17 +3968,17 @@ int sh_sample_blocks(uint64_t seed, uint64_t round, int lo, int count, int strid
 }  // extern "C"
 
 namespace {
-template <int K, int MODE>
+template <int K, int MODE, bool TIMED = false>
 int launch_santa(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   const SantaLds L = santa_lds_layout(a.n, MODE, ctx->ng);
   if (L.total > 160 * 1024) return fail(SH_ERR_ARGS, "block too large for the LDS tile");
   static thread_local AttrCache attr;
   if (L.total > 64 * 1024 && attr.need(ctx->device, L.total)) {
-    HIP_TRY(hipFuncSetAttribute((const void *)santa_block_kernel<K, MODE>,
+    HIP_TRY(hipFuncSetAttribute((const void *)santa_block_kernel<K, MODE, TIMED>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total));
     attr.set(ctx->device, L.total);
   }
-  hipLaunchKernelGGL((santa_block_kernel<K, MODE>), dim3(B), dim3(SANTA_WG), L.total, s, a);
+  hipLaunchKernelGGL((santa_block_kernel<K, MODE, TIMED>), dim3(B), dim3(SANTA_WG), L.total, s, a);
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
@@ -3944,8 +4128,10 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
       hipLaunchKernelGGL(santa_sp2_kernel<false>, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
                          (const unsigned char *)ctx->d_rec);
     else
-      hipLaunchKernelGGL(santa_sp3_kernel, dim3(B), dim3(WAVE), sp3_lds_layout().total, s, a,
-                         (const unsigned char *)ctx->d_rec);
+      if (a.flags & SH_FLAG_TIMING)
+        hipLaunchKernelGGL(santa_sp3_kernel<true>, dim3(B), dim3(WAVE), 0, s, a, (const unsigned char *)ctx->d_rec);
+      else
+        hipLaunchKernelGGL(santa_sp3_kernel<false>, dim3(B), dim3(WAVE), 0, s, a, (const unsigned char *)ctx->d_rec);
   } else if (vec)
     hipLaunchKernelGGL(santa_sp_kernel<true>, dim3(B), dim3(WAVE), lds, s, a);
   else
@@ -4057,7 +4243,7 @@ int resident_blocks(sh_ctx *ctx, int design, int mode, int n, int B) {
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
     case SH_DESIGN_VT_TILE: return vt_tile_slots(ctx);
     case SH_DESIGN_SPARSE2: return occ_blocks(ctx, santa_sp2_kernel<false>, WAVE, sp2_lds_layout().total);
-    case SH_DESIGN_SPARSE3: return occ_blocks(ctx, santa_sp3_kernel, WAVE, sp3_lds_layout().total);
+    case SH_DESIGN_SPARSE3: return occ_blocks(ctx, santa_sp3_kernel<false>, WAVE, 0);
     default:
       return occ_blocks(ctx, santa_sp_kernel<true>, WAVE, sp_lds_layout(ctx->ng, sp_capacity(ctx)).total);
   }
@@ -4092,7 +4278,8 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
              : mode == SH_MODE_TWINS ? launch_santa_big<1>(ctx, a, B, s)
                                      : launch_santa_big<2>(ctx, a, B, s);
     case SH_DESIGN_TWINS: return launch_santa<1, 1>(ctx, a, B, s);
-    case SH_DESIGN_LDS_TILE: return launch_santa<1, 0>(ctx, a, B, s);
+    case SH_DESIGN_LDS_TILE:
+      return (flags & SH_FLAG_TIMING) ? launch_santa<1, 0, true>(ctx, a, B, s) : launch_santa<1, 0>(ctx, a, B, s);
     case SH_DESIGN_VT_TILE: return launch_santa_vt_sc(ctx, a, B, s);
     case SH_DESIGN_SPARSE2:
     case SH_DESIGN_SPARSE3: return launch_santa_sp(ctx, a, B, s, true);

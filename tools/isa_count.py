@@ -39,7 +39,7 @@ for i, l in enumerate(body):
 # loops: the last branch back to a loop header label (the header's comment
 # names its depth); counted from the header to that back-edge
 heads = {lab: i for lab, i in labels.items()
-         if i + 1 < len(body) and "Loop Header" in " ".join(body[i:i + 2])}
+         if "Loop Header" in " ".join(body[i:i + 5])}
 last_back = {}
 for i, l in enumerate(body):
     t = l.strip().split()
@@ -54,3 +54,5 @@ for tgt, i in sorted(last_back.items(), key=lambda x: heads[x[0]]):
                 if u and not u[0].startswith((".", ";")) and not u[0].endswith(":"):
                     c[kind(u[0])] += 1
             print(f"loop {tgt} depth {depth.group(1) if depth else '?'} lines {labels[tgt]}-{i}: {dict(c)}")
+            if tgt in sys.argv[3:]:
+                print("\n".join(x for x in body[labels[tgt]:i + 1] if not x.strip().startswith(";")))

@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--flags", type=int, default=0, help="extra SH_FLAG_* bits (8 = LDS tile)")
     ap.add_argument("--budget", type=int, default=0, help="sparse kernel LDS bytes per block (0 = default)")
     ap.add_argument("--timing", action="store_true", help="per-phase in-kernel timing (sparse kernel)")
+    ap.add_argument("--segments", action="store_true",
+                    help="santa_sp3_kernel: shader cycles per Dijkstra step by segment (A fetch+scatter+LDS, "
+                         "B relax+argmin, C decode+book-keeping, D per-Dijkstra work per step)")
     ap.add_argument("--state-round", type=int, default=0,
                     help="time round R of the optimisation: first apply rounds 0..R-1 (default kernel)")
     a = ap.parse_args()
@@ -83,6 +86,17 @@ def main():
         out["timing_us"]["cycles_per_step"] = float(solve_cycles.sum() / sv.sum())
         imax = int(sv.argmax())
         out["timing_us"]["cycles_per_step_maxblock"] = float(solve_cycles[imax] / sv[imax])
+    if a.segments:
+        t = base.clone()
+        col = torch.zeros(B * a.n, dtype=torch.int32, device="cuda")
+        ctx.solve_blocks(a.mode, rows, a.n, t, steps=steps, col=col, flags=_lib.SH_FLAG_TIMING | a.flags)
+        cv = col.view(B, a.n)[:, :4].cpu().numpy().astype(float)
+        sv = steps.cpu().numpy().astype(float)
+        imax = int(sv.argmax())
+        names = ["A_fetch_scatter_lds", "B_relax_argmin", "C_decode_bookkeeping", "D_per_dijkstra"]
+        out["segments_cycles_per_step"] = {nm: float(cv[:, q].sum() / sv.sum()) for q, nm in enumerate(names)}
+        out["segments_cycles_per_step_maxblock"] = {nm: float(cv[imax, q] / sv[imax])
+                                                    for q, nm in enumerate(names)}
     out["blocks"] = B
     out["budget"] = a.budget
     out["cap"] = cap

@@ -23,7 +23,7 @@ def pmc(path):
 
 
 def short(name):
-    for key in ("santa_sp2_kernel", "santa_tile_kernel", "santa_sp_kernel", "santa_vt_kernel", "santa_sw_kernel", "santa_block_kernel",
+    for key in ("santa_sp3_kernel", "santa_sp2_kernel", "santa_tile_kernel", "santa_sp_kernel", "santa_vt_kernel", "santa_sw_kernel", "santa_block_kernel",
                 "santa_big_kernel", "score_kernel",
                 "sample_kernel", "lsap_i64_kernel", "lsap_f64_kernel"):
         if key in name:
@@ -37,7 +37,7 @@ def main(src, tag, root):
     stats = glob.glob(os.path.join(src, "trace_kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    for part in ("fetch", "write", "sq1", "sq2", "fetch_score"):
+    for part in ("fetch", "write", "sq1", "sq2", "occ", "fetch_score"):
         f = os.path.join(src, f"{part}_counter_collection.csv")
         if os.path.exists(f):
             shutil.copy(f, os.path.join(prof, f"{tag}_pmc_{part}.csv"))
@@ -60,7 +60,7 @@ def main(src, tag, root):
         w, k = b["warmup"], b["steps"]
         kn = b["roofline"]["kernel"].split(" ")[0].split("<")[0]
         # the register-tile sparse design runs two kernels per solve launch
-        kns = ["santa_tile_kernel", kn] if kn == "santa_sp2_kernel" else [kn]
+        kns = ["santa_tile_kernel", kn] if kn in ("santa_sp2_kernel", "santa_sp3_kernel") else [kn]
         vs = [trace.get(x, []) for x in kns]
         if all(len(v) >= w + k for v in vs):
             t = [sum(v[i] for v in vs) for i in range(w, w + k)]
@@ -94,6 +94,30 @@ def main(src, tag, root):
         sqs[short(k)] = e
     out["sq"] = sqs
     out["probe"] = probe
+    # occupancy and LDS activity (own PMC pass, tools/profile_round.sh "occ"):
+    #   mean resident waves per SIMD over the launch = SQ_WAVE_CYCLES (quad-
+    #   cycles, x4) / (GRBM_GUI_ACTIVE / 8 XCDs) / (CUs x 4 SIMDs), the
+    #   OccupancyPercent formula of rocprofv3's derived counters;
+    #   LDS-array busy = SQ_LDS_IDX_ACTIVE / (GRBM_GUI_ACTIVE / 8 x CUs);
+    #   conflict share = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE.
+    n_cu = 256
+    occ = {}
+    for k, v in pmc(os.path.join(src, "occ_counter_collection.csv")).items():
+        grbm = v.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+        if not grbm:
+            continue
+        e = {"kernel_cycles_per_xcd": grbm,
+             "mean_waves_per_simd": 4.0 * v.get("SQ_WAVE_CYCLES", 0.0) / grbm / (n_cu * 4)}
+        if v.get("SQ_LDS_IDX_ACTIVE"):
+            e["lds_array_busy_frac"] = v["SQ_LDS_IDX_ACTIVE"] / (grbm * n_cu)
+            e["lds_bank_conflict_frac"] = v.get("SQ_LDS_BANK_CONFLICT", 0.0) / v["SQ_LDS_IDX_ACTIVE"]
+            e["lds_insts"] = v.get("SQ_INSTS_LDS", 0.0)
+        occ[short(k)] = e
+    if occ:
+        out["occupancy_lds"] = occ
+    po = os.path.join(src, "probe_occ.json")
+    if os.path.exists(po):
+        out["probe_occ"] = json.loads(open(po).read().strip().splitlines()[-1])
     json.dump(out, open(os.path.join(prof, f"{tag}_summary.json"), "w"), indent=1)
     print(json.dumps(out["trace_ms"], indent=1))
     print(json.dumps(hbm, indent=1))
