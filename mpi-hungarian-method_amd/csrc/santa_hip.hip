@@ -1709,6 +1709,11 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
 }
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+
+// LDS byte address of a __shared__ object (for ds_* operands in inline asm)
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // slot of column j = 4*lane + k in the row buffer: the two 16-byte halves a
@@ -2996,7 +3001,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   const int mW = (Mm - 1) / 3, mU = Mm - 1 - mW;  // |m(W)| + |m(u~)| + 1 <= M
   __syncthreads();
   __builtin_amdgcn_s_setprio(3);  // (lowered over the last Dijkstras, below)
-  uint64_t tA = 0, tB = 0, tC = 0, tD = 0, ts = 0;
+  uint64_t tA = 0, tB = 0, tC = 0, tD = 0, tA1 = 0, ts = 0;
   auto stamp = [&](uint64_t &acc) {
     if constexpr (TIMED) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -3026,6 +3031,12 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   bool bad = (a.flags & SH_FLAG_TEST_RANGE) != 0;  // the lattice range left (per-lane flag)
   uint32_t accm = 0, acca = 0;                     // range of every u~ a step read (see below)
   const int l4 = 4 * lane;
+  // this lane's two row-buffer words (columns 4l, 4l+1 and 4l+2, 4l+3): kept
+  // in registers across the loop (recomputed per step into a register still
+  // read by the pending scatter, they made the compiler wait for it)
+  int ro0 = 2 * lane;
+  asm volatile("" : "+v"(ro0));
+  const uint32_t rob = lds_addr(rowc) + 4u * (uint32_t)ro0;  // (LDS byte address)
   if (a.flags & SH_FLAG_BUILD_ONLY) {
     c4r = (uint32_t)(4 * lane) * 0x01010101u + 0x03020100u;
   } else {
@@ -3062,44 +3073,80 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         stamp(first ? tD : tC);
         first = false;
         const uint32_t tw = tile2_get(T0, T1, i >> 2);
-        const int32_t uraw = u_l[i];
-        const int mover_v = rem[nrem - 1];  // the column at the last position
         const uint32_t e = (tw >> ((i & 1) << 4)) & 0xFFFFu;
         // the row's half of the wave (lanes 32L.., L = (i >> 1) & 1) as an SGPR mask
         const uint32_t hl = (uint32_t)(-((i >> 1) & 1));
         const bool mine = __builtin_amdgcn_inverse_ballot_w64(((uint64_t)hl << 32) | ~hl);
         const uint32_t ea = e >> 9;
-        // book-keeping: the winner first (its tie bits are unique while it is
-        // live; the mover's new bits may equal them), then the mover (a no-op
-        // when the mover is the winner: kX = 0)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          lo[k] = (lo[k] == pglo) ? ~0u : lo[k];
-          lo[k] ^= (l4 + k == mv) ? kX : 0u;
-        }
         // expand the row: hit columns get -a * 512, the rest hold a miss (1);
         // read this lane's four columns; put the misses back (in-order LDS)
         const int sslot = mine ? (int)(e & 0x1FFu) : 256 + x31;
-        rowc[sslot] = -(int32_t)(ea << 9);
+        const int32_t sval = -(int32_t)(ea << 9);
+        if constexpr (TIMED) {  // (A1: the tile fetch and the entry's fields)
+          asm volatile("" ::"v"(sslot), "v"(sval));
+          stamp(tA1);
+        }
+        int32_t uraw;
+        int mover_v;  // the column at the last position of `remaining`
         int2 c01, c23;
         // (a row with more than 32 hits has the marker in its entry 31: one
         // test for the whole slow path; the other half's marker only sends a
         // row without overflow through it, count 0)
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(ea == SP2_MARK) != 0, 0)) {
+          uraw = u_l[i];
+          mover_v = rem[nrem - 1];
+          rowc[sslot] = sval;
           const uint32_t rg = ovfr[i];
           const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
           for (int x = lane; x < oc; x += WAVE) {
             const uint32_t e2 = ovf[os + x];
             rowc[e2 & 0x1FFu] = -(int32_t)((e2 >> 9) << 9);
           }
-          c01 = *(const int2 *)(rowc + 2 * lane);
-          c23 = *(const int2 *)(rowc + 128 + 2 * lane);
+          c01 = *(const int2 *)(rowc + ro0);
+          c23 = *(const int2 *)(rowc + 128 + ro0);
           rowc[sslot] = 1;
           for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = 1;
+          // book-keeping of the previous step: the winner first (its tie bits
+          // are unique while it is live; the mover's new bits may equal them),
+          // then the mover (a no-op when the mover is the winner: kX = 0)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            lo[k] = (lo[k] == pglo) ? ~0u : lo[k];
+            lo[k] ^= (l4 + k == mv) ? kX : 0u;
+          }
         } else {
-          c01 = *(const int2 *)(rowc + 2 * lane);
-          c23 = *(const int2 *)(rowc + 128 + 2 * lane);
-          rowc[sslot] = 1;
+          // The step's LDS traffic as one issue group: the dual and the mover,
+          // the scatter, the row reads, the un-scatter -- no wait in between
+          // (compiled, the reads waited on earlier accesses whose address
+          // registers they reused); one wait below, after the book-keeping.
+          // Operands stay live through that wait.
+          const uint32_t ua = lds_addr(u_l) + 4u * (uint32_t)i;
+          const uint32_t ra = lds_addr(rem) + (uint32_t)(nrem - 1);
+          const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
+          const uint32_t one = 1;
+          asm volatile(
+              "ds_read_b32 %0, %8\n\t"
+              "ds_read_u8 %1, %9\n\t"
+              "ds_write_b32 %10, %11\n\t"
+              "ds_read2_b32 %2, %12 offset1:1\n\t"
+              "ds_read2_b32 %3, %12 offset0:128 offset1:129\n\t"
+              "ds_write_b32 %10, %13"
+              : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "+v"(lo[0]), "+v"(lo[1]),
+                "+v"(lo[2]), "+v"(lo[3])
+              : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(one)
+              : "memory");
+          // book-keeping of the previous step (as the slow path's), in the
+          // shadow of the LDS accesses
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            lo[k] = (lo[k] == pglo) ? ~0u : lo[k];
+            lo[k] ^= (l4 + k == mv) ? kX : 0u;
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(uraw), "+v"(mover_v), "+v"(c01), "+v"(c23), "+v"(lo[0]), "+v"(lo[1]),
+                         "+v"(lo[2]), "+v"(lo[3])
+                       : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(one)
+                       : "memory");
         }
         const int32_t cc[4] = {c01.x, c01.y, c23.x, c23.y};
         // u~[i] = u[i] - minVal (row i is reached at the current minimum)
@@ -3141,13 +3188,11 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         mv = mover_v;
         rem[pstar] = (uint8_t)mover_v;  // (every lane, same byte; a no-op when pstar == last)
         --nrem;
-        // (branch-free: the row is read either way, used when assigned)
-        const int nxt = (int)((__builtin_amdgcn_readlane((int)r4c, lw) >> (8 * kw)) & 0xFFu);
-        if (!assigned) {
-          sink = 4 * lw + kw;
-          break;
-        }
-        i = nxt;
+        // (branch-free: both the winner's column and its row are formed; the
+        // row is the next step's when assigned, the column is the sink if not)
+        sink = 4 * lw + kw;
+        i = (int)((__builtin_amdgcn_readlane((int)r4c, lw) >> (8 * kw)) & 0xFFu);
+        if (!assigned) break;
       }
       // Dual update (santa_sp2_kernel's, in V units): the columns that left
       // `remaining` (lo = ~0; not the sink, whose update is 0) add
@@ -3242,9 +3287,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   if (lane == 0) {
     if (a.cost) a.cost[b] = cost;
     if (a.steps) a.steps[b] = steps;
-    if (TIMED && a.col && n >= 4) {
-      const uint64_t seg[4] = {tA, tB, tC, tD};
-      for (int q = 0; q < 4; ++q) a.col[(size_t)b * n + q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
+    if (TIMED && a.col && n >= 5) {
+      const uint64_t seg[5] = {tA, tB, tC, tD, tA1};
+      for (int q = 0; q < 5; ++q) a.col[(size_t)b * n + q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
     }
     if (a.delta) {
       atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
