@@ -27,8 +27,8 @@ for s in "$@"; do
     probe) step probe_sp 180 python -u tools/probe.py --reps 3 &&
            step probe_vt 180 python -u tools/probe.py --reps 3 --flags 32 ;;
     bench) step bench 600 python -u bench.py ;;
-    bench_twins) step bench_twins 600 python -u bench.py --mode twins --no-cpu-baseline ;;
-    bench_triplets) step bench_triplets 600 python -u bench.py --mode triplets --no-cpu-baseline ;;
+    bench_twins) step bench_twins 600 python -u bench.py --mode twins ;;
+    bench_triplets) step bench_triplets 600 python -u bench.py --mode triplets ;;
     bench_n2000) step bench_n2000 600 python -u bench.py --n 2000 --steps 5 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
