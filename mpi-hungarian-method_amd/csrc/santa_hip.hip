@@ -379,6 +379,11 @@ constexpr uint64_t KEY_HI_MAX = (1ull << 43) - 1;
 constexpr int64_t KEY_BIAS = 1ll << 42;
 constexpr uint64_t SIGN64 = 0x8000000000000000ull;
 
+// LDS byte address of a __shared__ object (for ds_* operands in inline asm)
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
 struct SolveLds {
   int64_t *u;       // [n]   row duals
   int16_t *c4r;     // [n]   col4row (the result)
@@ -611,6 +616,9 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
   uint32_t lo = 0;
   int64_t steps = 0;
   int par = 0;  // rotating step-argmin word (0..2), as sap_solve_mw
+  const uint32_t wbase = lds_addr(S.red);
+  uint64_t ones = ~0ull;
+  asm volatile("" : "+v"(ones));
   if (tid < 3) S.red[tid] = ~0ull;
   __syncthreads();
   for (int cur = 0; cur < n; ++cur) {
@@ -623,29 +631,69 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
     int64_t minVal = 0;
     int i = cur;
     int sink;
+    // the previous step's winner position (leaves `remaining`) and its mover
+    // (position `last` -> pstar), applied at the top of the next step in the
+    // shadow of its row and dual loads (sap_solve_mw_l32's schedule)
+    int pstar = -2, last = -3;
+    uint32_t kX = 0;
     for (;;) {
       ++steps;
       const uint64_t uraw = (uint64_t)S.u[i];
       int64_t c[1];
       ld.load(i, c, la...);
-      if (tid == 0) S.red[par == 2 ? 0 : par + 1] = ~0ull;
+      {
+        // re-arm the next step's word: lane 0 of every wave writes ~0 (the
+        // word was last read before barrier t - 1, is next folded after
+        // barrier t; the fold's wait below covers this write)
+        const uint32_t wn = wbase + 8u * (uint32_t)(par == 2 ? 0 : par + 1);
+        uint64_t sv;
+        asm volatile(
+            "s_mov_b64 %0, exec\n\t"
+            "s_mov_b64 exec, 1\n\t"
+            "ds_write_b64 %1, %2\n\t"
+            "s_mov_b64 exec, %0"
+            : "=&s"(sv)
+            : "v"(wn), "v"(ones)
+            : "memory");
+      }
+      {
+        const bool isW = pos == pstar, isM = pos == last;
+        lo ^= isM ? kX : 0u;  // (kX = 0 when the mover is the winner)
+        pos = isW ? -1 : (isM ? pstar : pos);
+      }
       const int64_t ui = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uraw >> 32)) << 32) |
                                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)uraw));
       uint64_t bse = SC_BIAS - (uint64_t)(ui - minVal);
       asm volatile("" : "+s"(bse));  // one SGPR pair: (W + c) + bse
       const bool act = pos >= 0;
+      // (a removed column never improves: r >= minVal >= its spc)
       const int64_t r = (int64_t)((uint64_t)(W + c[0]) + bse);
-      const bool upd = act && (r < sb);
+      const bool upd = r < sb;
       sb = upd ? r : sb;
       path = upd ? i : path;
       const uint64_t best = act ? ((uint64_t)sb | lo) : ~0ull;
       const uint32_t bh = (uint32_t)(best >> 32);
       // DPP min of the high words within each 16-lane row (every lane holds its
-      // row's minimum, no row_bcast steps or readlane); the lanes holding it
-      // (usually one per row) fold their full keys into the step word
+      // row's minimum); the lanes holding it fold their full keys into the step
+      // word: the exec mask set around one ds_min_u64, no branch (the wait for
+      // the atomic is in the asm: the compiler's waitcnt before the barrier
+      // does not see LDS ops issued by inline asm)
       const uint32_t mh = row_min_u32_dpp(bh);
-      if (bh == mh && mh != ~0u)
-        __hip_atomic_fetch_min(S.red + par, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      {
+        const uint32_t wa = wbase + 8u * (uint32_t)par;
+        uint64_t sv, m0, m1;
+        asm volatile(
+            "v_cmp_eq_u32_e64 %1, %3, %4\n\t"
+            "v_cmp_ne_u32_e64 %2, -1, %4\n\t"
+            "s_and_b64 %1, %1, %2\n\t"
+            "s_and_saveexec_b64 %0, %1\n\t"
+            "ds_min_u64 %5, %6\n\t"
+            "s_mov_b64 exec, %0\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&s"(sv), "=&s"(m0), "=&s"(m1)
+            : "v"(bh), "v"(mh), "v"(wa), "v"(best)
+            : "memory");
+      }
       __syncthreads();
       const uint64_t g = S.red[par];
       par = (par == 2) ? 0 : par + 1;
@@ -656,16 +704,19 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
       const bool assigned = (glo >> 16) & 1u;
       const int pk = (int)((glo >> 8) & 255u);
       const int aux = (int)(glo & 255u);
-      const int pstar = assigned ? pk : 255 - pk;
-      const int last = nrem - 1;
-      lo ^= (pos == last) ? ((uint32_t)(last ^ pstar) << 8) : 0u;  // the mover's position key
-      pos = (pos == pstar) ? -1 : ((pos == last) ? pstar : pos);
+      pstar = assigned ? pk : 255 - pk;
+      last = nrem - 1;
+      kX = (uint32_t)(last ^ pstar) << 8;
       --nrem;
       if (!assigned) {
         sink = aux;
         break;
       }
       i = aux;
+    }
+    {  // the last step's book-keeping (the sink leaves `remaining`)
+      const bool isW = pos == pstar, isM = pos == last;
+      pos = isW ? -1 : (isM ? pstar : pos);
     }
     big |= (uint64_t)(minVal + SC_LIM) >= 2 * (uint64_t)SC_LIM;
     // dual update and path dump (sap_solve_mw's, in scaled units)
@@ -731,10 +782,11 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
   int32_t *u32 = (int32_t *)S.u;
   const int Mm = (int)min((int64_t)199, (int64_t)(0xFFFFFFFFll / E) / 2);
   const int mW = (Mm - 1) / 3, mU = Mm - 1 - mW;
+  const uint32_t wa = lds_addr(S.red);  // the step word (LDS byte address)
   uint32_t sb = SP3_INF;
   int32_t W = 0;  // -v (this thread's column)
   int path = -1, pos = -1, r4c = -1;
-  uint32_t lo = 0, aux = 0;
+  uint32_t lo = ~0u;  // key tie-break bits; ~0: left `remaining` (or j >= n)
   uint32_t accm = 0, acca = 0;
   int steps = 0;
   uint64_t tA = 0, tB = 0, tC = 0, tD = 0, ts = 0;
@@ -753,12 +805,17 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
     sb = SP3_INF;
     pos = colv ? (n - 1 - j) : -1;
     r4c = colv ? S.r4c[j] : -1;
-    lo = (r4c < 0) ? ((255u - (uint32_t)pos) << 2) : (((1u << 8) | (uint32_t)pos) << 2);
-    aux = (r4c < 0) ? (uint32_t)j : (uint32_t)r4c;
+    lo = !colv ? ~0u : (r4c < 0) ? ((255u - (uint32_t)pos) << 2) : (((1u << 8) | (uint32_t)pos) << 2);
+    const uint32_t aux = (r4c < 0) ? (uint32_t)j : (uint32_t)r4c;
     int nrem = n;
     int32_t minVal = 0;
     int i = cur;
     int sink;
+    // the previous step's winner position (leaves `remaining`) and its mover
+    // (the column at position `last` takes position pstar): applied at the top
+    // of the next step, in the shadow of its row and dual loads
+    int pstar = -2, last = -3;
+    uint32_t kX = 0;
     bool first = true;
     for (;;) {
       ++steps;
@@ -767,6 +824,14 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
       const int32_t uraw = u32[i];
       int32_t c;
       ld.load(i, c, la...);
+      // (an LDS-tile row: the previous step's book-keeping here, in the shadow
+      // of the loads; a register-tile row is a VALU/SALU chain with nothing to
+      // hide behind: its book-keeping stays at the end of the step, below)
+      if constexpr (!Loader::kReg) {
+        const bool isW = pos == pstar, isM = pos == last;
+        lo = isW ? ~0u : (isM ? (lo ^ kX) : lo);
+        pos = isW ? -1 : (isM ? pstar : pos);
+      }
       const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
       if constexpr (TIMED) {
         asm volatile("" ::"v"(c), "s"(ui));
@@ -774,37 +839,67 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
       }
       accm = max(accm, (uint32_t)(ui + mU) & 511u);
       acca = max(acca, (uint32_t)(ui < 0 ? -ui : ui));
-      const uint32_t bse = (uint32_t)(SP3_BIAS - ui);
-      const bool act = pos >= 0;
+      uint32_t bse = (uint32_t)(SP3_BIAS - ui);
+      asm volatile("" : "+s"(bse));
+      // (a removed column never improves: r >= minVal >= its spc; a column
+      // j >= n has lo = ~0, so its key is ~0 whatever sb holds)
       const uint32_t r = (uint32_t)W + (uint32_t)c + bse;
-      const bool upd = act && (r < sb);
+      const bool upd = r < sb;
       sb = upd ? r : sb;
       path = upd ? i : path;
-      const uint32_t key = act ? ((sb << SP3_SH) | lo) : ~0u;
-      // row minimum (every lane holds its 16-lane row's), its holders fold
-      // (tag, key, aux) into the step word
+      const uint32_t key = (sb << SP3_SH) | lo;
+      // the 64-bit step word (0xFFFF - step) << 48 | key << 16 | aux, formed
+      // before the row minimum is known (off the chain)
+      const uint32_t tag = 0xFFFFu - (uint32_t)steps;
+      const uint64_t word = ((uint64_t)__builtin_amdgcn_alignbit(tag, key, 16) << 32) | ((key << 16) | aux);
+      // row minimum (every lane holds its 16-lane row's); its holders fold the
+      // word into the step word: the exec mask set around one ds_min_u64, no branch
       const uint32_t mh = row_min_u32_dpp(key);
-      if (key == mh && mh != ~0u)
-        __hip_atomic_fetch_min(S.red, ((uint64_t)(0xFFFFu - (uint32_t)steps) << 48) | ((uint64_t)key << 16) | aux,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      {
+        // (the wait for the atomic is in the asm: the compiler's waitcnt
+        // before the barrier does not see LDS ops issued by inline asm)
+        uint64_t sv, m0, m1;
+        asm volatile(
+            "v_cmp_eq_u32_e64 %1, %3, %4\n\t"
+            "v_cmp_ne_u32_e64 %2, -1, %4\n\t"
+            "s_and_b64 %1, %1, %2\n\t"
+            "s_and_saveexec_b64 %0, %1\n\t"
+            "ds_min_u64 %5, %6\n\t"
+            "s_mov_b64 exec, %0\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&s"(sv), "=&s"(m0), "=&s"(m1)
+            : "v"(key), "v"(mh), "v"(wa), "v"(word)
+            : "memory");
+      }
       stamp(tB);
       __syncthreads();
       const uint64_t g = S.red[0];
-      const uint32_t gk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 16));
-      const int ga = __builtin_amdgcn_readfirstlane((int)(uint32_t)g) & 0xFF;
+      const uint32_t glo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
+      const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32));
+      const int ga = (int)(glo & 0xFFu);
+      const uint32_t gk = (ghi << 16) | (glo >> 16);
       minVal = (int32_t)(gk >> SP3_SH) - SP3_BIAS;
       const bool assigned = (gk >> 10) & 1u;
       const int pk = (int)((gk >> 2) & 255u);
-      const int pstar = assigned ? pk : 255 - pk;
-      const int last = nrem - 1;
-      lo ^= (pos == last) ? ((uint32_t)(last ^ pstar) << 2) : 0u;  // the mover's position key
-      pos = (pos == pstar) ? -1 : ((pos == last) ? pstar : pos);
+      pstar = assigned ? pk : 255 - pk;
+      last = nrem - 1;
+      kX = (uint32_t)(last ^ pstar) << 2;
       --nrem;
+      if constexpr (Loader::kReg) {
+        const bool isW = pos == pstar, isM = pos == last;
+        lo = isW ? ~0u : (isM ? (lo ^ kX) : lo);
+        pos = isW ? -1 : (isM ? pstar : pos);
+      }
       if (!assigned) {
         sink = ga;
         break;
       }
       i = ga;
+    }
+    if constexpr (!Loader::kReg) {  // the last step's book-keeping (the sink leaves `remaining`)
+      const bool isW = pos == pstar, isM = pos == last;
+      lo = isW ? ~0u : (isM ? (lo ^ kX) : lo);
+      pos = isW ? -1 : (isM ? pstar : pos);
     }
     // dual update and path dump (sap_solve_mw_sc's, in V units)
     if (colv && pos < 0) {
@@ -859,6 +954,7 @@ struct TileU8Loader {  // singles: uint8 rank codes, row stride RS bytes (costs 
 };
 
 struct TileU8LoaderV {  // singles: uint8 rank codes -> lattice V (a wish -a * 512, a miss 1)
+  static constexpr bool kReg = false;  // (an LDS load: work placed after it hides in its latency)
   const uint8_t *tile;
   int RS, nw1;
   __device__ __forceinline__ void load(int i, int32_t &c) const {
@@ -1361,6 +1457,7 @@ struct VtRegLoader {
 };
 
 struct VtRegLoaderV {  // VtRegLoader's code -> lattice V (santa_sp3_kernel's units)
+  static constexpr bool kReg = true;  // (register moves: nothing to hide behind)
   int nw1;
   __device__ __forceinline__ void load(int i, int32_t &c, const u32x32 &ta, const u32x32 &tb) const {
     const int d = i >> 2;
@@ -1710,10 +1807,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 
-// LDS byte address of a __shared__ object (for ds_* operands in inline asm)
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
-}
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
 // slot of column j = 4*lane + k in the row buffer: the two 16-byte halves a
@@ -3031,6 +3124,12 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   bool bad = (a.flags & SH_FLAG_TEST_RANGE) != 0;  // the lattice range left (per-lane flag)
   uint32_t accm = 0, acca = 0;                     // range of every u~ a step read (see below)
   const int l4 = 4 * lane;
+  int colk[4];  // this lane's columns (VGPR constants for the book-keeping compares)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    colk[k] = l4 + k;
+    asm volatile("" : "+v"(colk[k]));
+  }
   // this lane's two row-buffer words (columns 4l, 4l+1 and 4l+2, 4l+3): kept
   // in registers across the loop (recomputed per step into a register still
   // read by the pending scatter, they made the compiler wait for it)
@@ -3089,12 +3188,65 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         int32_t uraw;
         int mover_v;  // the column at the last position of `remaining`
         int2 c01, c23;
-        // (a row with more than 32 hits has the marker in its entry 31: one
-        // test for the whole slow path; the other half's marker only sends a
-        // row without overflow through it, count 0)
+        // The step's LDS traffic as one issue group for every row (a row with
+        // more than 32 hits has the marker, whose slot is a dump slot, in its
+        // entry 31); such a row re-reads its columns below.  One path through
+        // the group keeps lo[] in one set of registers across the loop.
+        // The step's LDS traffic as one issue group: the dual and the mover,
+        // the scatter, the row reads, the un-scatter -- no wait in between
+        // (compiled, the reads waited on earlier accesses whose address
+        // registers they reused); one wait below, after the book-keeping.
+        // Operands stay live through that wait.
+        const uint32_t ua = lds_addr(u_l) + 4u * (uint32_t)i;
+        const uint32_t ra = lds_addr(rem) + (uint32_t)(nrem - 1);
+        const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
+        const uint32_t one = 1;
+        // book-keeping of the previous step (as the slow path's) in the
+        // shadow of the LDS accesses, in the same asm: lo[] is updated in
+        // place (computed in C++ the new values took new registers, copied
+        // back at the loop latch), the compares write SGPR pairs read 3+
+        // instructions later (no s_nop between compare and select)
+        uint64_t t0, t1, t2, t3;
+        uint32_t x0, x1, x2, x3;
+        asm volatile(
+            "ds_read_b32 %0, %14\n\t"
+            "ds_read_u8 %1, %15\n\t"
+            "ds_write_b32 %16, %17\n\t"
+            "ds_read2_b32 %2, %18 offset1:1\n\t"
+            "ds_read2_b32 %3, %18 offset0:128 offset1:129\n\t"
+            "ds_write_b32 %16, %19\n\t"
+            "v_cmp_ne_u32_e64 %8, %20, %4\n\t"
+            "v_cmp_ne_u32_e64 %9, %20, %5\n\t"
+            "v_cmp_ne_u32_e64 %10, %20, %6\n\t"
+            "v_cmp_ne_u32_e64 %11, %20, %7\n\t"
+            "v_cndmask_b32_e64 %4, -1, %4, %8\n\t"
+            "v_cndmask_b32_e64 %5, -1, %5, %9\n\t"
+            "v_cndmask_b32_e64 %6, -1, %6, %10\n\t"
+            "v_cndmask_b32_e64 %7, -1, %7, %11\n\t"
+            "v_cmp_eq_u32_e64 %8, %21, %23\n\t"
+            "v_cmp_eq_u32_e64 %9, %21, %24\n\t"
+            "v_cmp_eq_u32_e64 %10, %21, %25\n\t"
+            "v_cmp_eq_u32_e64 %11, %21, %26\n\t"
+            "v_cndmask_b32_e64 %12, 0, %22, %8\n\t"
+            "v_cndmask_b32_e64 %13, 0, %22, %9\n\t"
+            "v_xor_b32 %4, %4, %12\n\t"
+            "v_cndmask_b32_e64 %12, 0, %22, %10\n\t"
+            "v_xor_b32 %5, %5, %13\n\t"
+            "v_cndmask_b32_e64 %13, 0, %22, %11\n\t"
+            "v_xor_b32 %6, %6, %12\n\t"
+            "v_xor_b32 %7, %7, %13\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "+v"(lo[0]), "+v"(lo[1]),
+              "+v"(lo[2]), "+v"(lo[3]), "=&s"(t0), "=&s"(t1), "=&s"(t2), "=&s"(t3), "=&v"(x0), "=&v"(x1)
+            : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(one), "s"(pglo), "v"(mv), "v"(kX),
+              "v"(colk[0]), "v"(colk[1]), "v"(colk[2]), "v"(colk[3])
+            : "memory");
+        (void)x2;
+        (void)x3;
+        // (a row with more than 32 hits: the tile's entries and the overflow
+        // list scattered again, the four columns re-read; the other half's
+        // marker only sends a row without overflow through here, count 0)
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(ea == SP2_MARK) != 0, 0)) {
-          uraw = u_l[i];
-          mover_v = rem[nrem - 1];
           rowc[sslot] = sval;
           const uint32_t rg = ovfr[i];
           const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
@@ -3106,47 +3258,6 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           c23 = *(const int2 *)(rowc + 128 + ro0);
           rowc[sslot] = 1;
           for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = 1;
-          // book-keeping of the previous step: the winner first (its tie bits
-          // are unique while it is live; the mover's new bits may equal them),
-          // then the mover (a no-op when the mover is the winner: kX = 0)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            lo[k] = (lo[k] == pglo) ? ~0u : lo[k];
-            lo[k] ^= (l4 + k == mv) ? kX : 0u;
-          }
-        } else {
-          // The step's LDS traffic as one issue group: the dual and the mover,
-          // the scatter, the row reads, the un-scatter -- no wait in between
-          // (compiled, the reads waited on earlier accesses whose address
-          // registers they reused); one wait below, after the book-keeping.
-          // Operands stay live through that wait.
-          const uint32_t ua = lds_addr(u_l) + 4u * (uint32_t)i;
-          const uint32_t ra = lds_addr(rem) + (uint32_t)(nrem - 1);
-          const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
-          const uint32_t one = 1;
-          asm volatile(
-              "ds_read_b32 %0, %8\n\t"
-              "ds_read_u8 %1, %9\n\t"
-              "ds_write_b32 %10, %11\n\t"
-              "ds_read2_b32 %2, %12 offset1:1\n\t"
-              "ds_read2_b32 %3, %12 offset0:128 offset1:129\n\t"
-              "ds_write_b32 %10, %13"
-              : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "+v"(lo[0]), "+v"(lo[1]),
-                "+v"(lo[2]), "+v"(lo[3])
-              : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(one)
-              : "memory");
-          // book-keeping of the previous step (as the slow path's), in the
-          // shadow of the LDS accesses
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            lo[k] = (lo[k] == pglo) ? ~0u : lo[k];
-            lo[k] ^= (l4 + k == mv) ? kX : 0u;
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)"
-                       : "+v"(uraw), "+v"(mover_v), "+v"(c01), "+v"(c23), "+v"(lo[0]), "+v"(lo[1]),
-                         "+v"(lo[2]), "+v"(lo[3])
-                       : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(one)
-                       : "memory");
         }
         const int32_t cc[4] = {c01.x, c01.y, c23.x, c23.y};
         // u~[i] = u[i] - minVal (row i is reached at the current minimum)
@@ -3171,6 +3282,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           const uint32_t key = (sb[k] << SP3_SH) | lo[k];  // (removed: lo = ~0)
           best = key < best ? key : best;
         }
+        // the row of this lane's best column (byte best & 3 of r4c): formed in
+        // the DPP chain's wait states, one readlane of it below gives the next row
+        const uint32_t rsel = (r4c >> ((best & 3u) << 3)) & 0xFFu;
         const uint32_t g = wave_min_u32_dpp(best);
         if constexpr (TIMED) {
           asm volatile("" ::"s"(g));
@@ -3191,7 +3305,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         // (branch-free: both the winner's column and its row are formed; the
         // row is the next step's when assigned, the column is the sink if not)
         sink = 4 * lw + kw;
-        i = (int)((__builtin_amdgcn_readlane((int)r4c, lw) >> (8 * kw)) & 0xFFu);
+        i = __builtin_amdgcn_readlane((int)rsel, lw);
         if (!assigned) break;
       }
       // Dual update (santa_sp2_kernel's, in V units): the columns that left
