@@ -375,7 +375,6 @@ __device__ __forceinline__ uint64_t wave_min_u64_fast(uint64_t x) {
 }
 
 constexpr int KEY_LO_BITS = 21;
-constexpr uint64_t KEY_HI_MAX = (1ull << 43) - 1;
 constexpr int64_t KEY_BIAS = 1ll << 42;
 constexpr uint64_t SIGN64 = 0x8000000000000000ull;
 
@@ -964,25 +963,57 @@ struct TileU8LoaderV {  // singles: uint8 rank codes -> lattice V (a wish -a * 5
 };
 
 constexpr int TWIN_LUT = 1024;  // 3 classes x 256, padded to the 10-bit index mask
+
+// Twins tile entries of the 4-wave kernel, re-coded after the build from the
+// code pair (c1 | c2 << 8), so that a Dijkstra step decodes its cost with a
+// few VALU instead of a dependent LDS table read (round 2's cost table):
+//   a (8 bits) | k (5) << 8 | up (1) << 13 | dbl (1) << 14,
+//   m = ((E & -2^k) + up * 2^k) << dbl,   cost = -a * 2^32 + m   (units).
+// One hit (cls 1): k, up reproduce one_hit_residual(a, E) (E rounded to 2^k,
+// the rounding direction precomputed); both wish (cls 2): k = 31, m = 0;
+// neither (cls 0): k = 0, dbl, m = 2E.  a = a1 + a2 (wish values).  The
+// context checks the decode against twin_cost's arithmetic for every pair.
+__host__ __device__ __forceinline__ uint32_t twin_entry(uint32_t code16, int nw1, int64_t E) {
+  const uint32_t c1 = code16 & 0xFFu, c2 = code16 >> 8;
+  const uint32_t a = (c1 ? nw1 - c1 : 0u) + (c2 ? nw1 - c2 : 0u);
+  if (c1 && c2) return a | (31u << 8);
+  if (!(c1 | c2)) return 1u << 14;
+  const int k = 39 - __builtin_clz(2u * a - 1u);  // (p + 8 of one_hit_residual)
+  const int64_t q = (int64_t)1 << k;
+  const int64_t rem = E & (q - 1), base = E - rem, half = q >> 1;
+  const uint32_t up = (rem > half || (rem == half && ((base >> k) & 1))) ? 1u : 0u;
+  return a | ((uint32_t)k << 8) | (up << 13);
+}
+template <int SH>
+__host__ __device__ __forceinline__ int64_t twin_entry_cost(uint32_t e, uint32_t E32) {
+  const uint32_t a = e & 0xFFu, k = (e >> 8) & 31u, up = (e >> 13) & 1u, dbl = (e >> 14) & 1u;
+  const uint32_t q = 1u << k;
+  const uint32_t m = ((E32 & (0u - q)) + up * q) << dbl;
+  return (int64_t)(((uint64_t)m << SH) - ((uint64_t)a << (32 + SH)));
+}
+// child-side happiness of both twins: 2a (both wish), 2a - 1 (one), -2 (none)
+__device__ __forceinline__ int64_t twin_entry_happy(uint32_t e) {
+  const int cls = ((e >> 14) & 1u) ? 0 : ((((e >> 8) & 31u) == 31u) ? 2 : 1);
+  return 2 * (int64_t)(e & 0xFFu) - (2 - cls);
+}
+
 template <int NW, int K, int SH = 0>
-struct TileU16Loader {  // twins: uint16 cost-table indices, row stride RS elements (costs x 2^SH)
+struct TileU16Loader {  // twins: uint16 entries (twin_entry), row stride RS elements (costs x 2^SH)
+  static constexpr bool kReg = false;
   const uint16_t *tile;
-  const int64_t *lut;  // twin_lut_index -> exact cost (units), in LDS
+  uint32_t E32;
   int RS;
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint16_t *p = tile + (size_t)i * RS + w * (WAVE * K) + lane;
 #pragma unroll
-    for (int k = 0; k < K; ++k)  // (lanes past n read any row)
-      c[k] = (int64_t)((uint64_t)lut[p[k * WAVE] & (TWIN_LUT - 1)] << SH);
+    for (int k = 0; k < K; ++k)  // (lanes past n read any entry: any value, never used)
+      c[k] = twin_entry_cost<SH>(p[k * WAVE], E32);
   }
 };
 
-// Twins tile entries in the 4-wave kernel are re-coded after the build from
-// the code pair (c1 | c2 << 8) to idx = cls << 8 | a (cls = number of twins
-// wishing the column's gift, a = a1 + a2), so a Dijkstra step decodes a cost
-// with one LDS table read instead of the float32-rounding arithmetic of
-// twin_cost.  The table holds twin_cost of every (cls, a).
+// The large-block kernel's twins rows (santa_big_kernel, n > 256) still look
+// their cost up in an LDS table of every (cls, a): index cls << 8 | a.
 __device__ __forceinline__ uint32_t twin_lut_index(uint32_t code16, int nw1) {
   const uint32_t c1 = code16 & 0xFFu, c2 = code16 >> 8;
   const uint32_t a = (c1 ? nw1 - c1 : 0u) + (c2 ? nw1 - c2 : 0u);
@@ -992,10 +1023,6 @@ __device__ __forceinline__ int64_t twin_lut_cost(uint32_t idx, int64_t E) {
   const int cls = (int)(idx >> 8), a = (int)(idx & 0xFFu);
   const int64_t m = cls == 2 ? 0 : (cls == 1 ? one_hit_residual(a, E) : 2 * E);
   return (int64_t)(-a) * 4294967296LL + m;
-}
-// child-side happiness of both twins: 2a (both wish), 2a - 1 (one), -2 (none)
-__device__ __forceinline__ int64_t twin_lut_happy(uint32_t idx) {
-  return 2 * (int64_t)(idx & 0xFFu) - (2 - (int64_t)(idx >> 8));
 }
 
 template <int NW, int K, typename S>
@@ -1081,7 +1108,7 @@ constexpr int SANTA_NW = 4;
 constexpr int SANTA_WG = SANTA_NW * WAVE;
 
 struct SantaLds {
-  size_t tile, u, rows, ctype, c4r, r4c, path, red, head, nxt, part, lut, total;
+  size_t tile, u, rows, ctype, c4r, r4c, path, red, head, nxt, part, total;
   int RS;
 };
 
@@ -1100,7 +1127,6 @@ __host__ __device__ __forceinline__ SantaLds santa_lds_layout(int n, int mode, i
   L.head = off;  off += r16((size_t)ng * 4);
   L.nxt = off;   off += r16((size_t)n * 2);
   L.part = off;  off += r16((size_t)SANTA_NW * 3 * 8);
-  L.lut = off;   off += mode ? (size_t)TWIN_LUT * 8 : 0;
   L.total = off;
   return L;
 }
@@ -1220,15 +1246,14 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
     S.r4c[i] = -1;
   }
   const int nw1 = a.n_wish + 1;
-  int64_t *lut = (int64_t *)(smem + L.lut);
-  if (MODE) {  // code pairs -> cost-table indices (see twin_lut_index)
-    for (int q = tid; q < TWIN_LUT; q += SANTA_WG) lut[q] = twin_lut_cost((uint32_t)q, a.E);
-    __syncthreads();
+  const uint32_t E32 = (uint32_t)a.E;
+  if (MODE) {  // code pairs -> decodable entries (see twin_entry)
+    __syncthreads();  // (the build's last code pairs)
     // (8 entries per 16-byte LDS access; n * RS is a multiple of 16)
     uint4 *t4 = (uint4 *)tile8;
     const int cnt4 = n * RS / 8;
     auto rc2 = [&](uint32_t w) -> uint32_t {
-      return twin_lut_index(w & 0xFFFFu, nw1) | (twin_lut_index(w >> 16, nw1) << 16);
+      return twin_entry(w & 0xFFFFu, nw1, a.E) | (twin_entry(w >> 16, nw1, a.E) << 16);
     };
     for (int q = tid; q < cnt4; q += SANTA_WG) {
       const uint4 v = t4[q];
@@ -1261,7 +1286,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
           redo = sap_solve_mw_l32<SANTA_NW, TIMED>(n, ld, S, steps, force, a.E, seg);
         }
       } else {
-        const TileU16Loader<SANTA_NW, 1, SC_SH> ld{(const uint16_t *)tile8, lut, RS};
+        const TileU16Loader<SANTA_NW, 1, SC_SH> ld{(const uint16_t *)tile8, E32, RS};
         redo = sap_solve_mw_sc<SANTA_NW>(n, ld, S, steps, force);
       }
     }
@@ -1276,7 +1301,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
         const TileU8Loader<SANTA_NW, K> ld{tile8, RS, nw1, a.E};
         sap_solve_mw<SANTA_NW, K>(n, ld, S, steps, fallbacks, exact);
       } else {
-        const TileU16Loader<SANTA_NW, K> ld{(const uint16_t *)tile8, lut, RS};
+        const TileU16Loader<SANTA_NW, K> ld{(const uint16_t *)tile8, E32, RS};
         sap_solve_mw<SANTA_NW, K>(n, ld, S, steps, fallbacks, exact);
       }
     }
@@ -1298,8 +1323,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
       const uint16_t *t16 = (const uint16_t *)tile8;
       const uint32_t cn = t16[(size_t)i * RS + col];
       const uint32_t co = t16[(size_t)i * RS + i];
-      cost += lut[cn & (TWIN_LUT - 1)];
-      dch += twin_lut_happy(cn) - twin_lut_happy(co);
+      cost += twin_entry_cost<0>(cn, E32);
+      dch += twin_entry_happy(cn) - twin_entry_happy(co);
       // (unconditional: guarding these reads on a.delta, as the other kernels do,
       // made this kernel 2 % slower in A/B bench runs -- code generation)
       dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
@@ -4051,6 +4076,17 @@ int sh_ctx_create(sh_ctx **out, int device, const int16_t *h_wish, int n_wish,
       if (units != (int64_t)(-a) * 4294967296LL + one_hit_residual(a, E))
         return fail(SH_ERR_ARGS, "twin cost decode mismatch");
     }
+    // the 4-wave twins kernel's tile entries (twin_entry) decode to the same costs
+    if (E <= 0 || E >= ((int64_t)1 << 31)) return fail(SH_ERR_ARGS, "miss value out of the entry decode's range");
+    const int nw1 = n_wish + 1;
+    for (int c1 = 0; c1 <= n_wish; ++c1)
+      for (int c2 = 0; c2 <= n_wish; ++c2) {
+        const int a1 = c1 ? nw1 - c1 : 0, a2 = c2 ? nw1 - c2 : 0, aa = a1 + a2;
+        const int64_t m = (c1 && c2) ? 0 : (c1 || c2) ? one_hit_residual(aa, E) : 2 * E;
+        const uint32_t e16 = twin_entry((uint32_t)c1 | ((uint32_t)c2 << 8), nw1, E);
+        if (e16 > 0xFFFFu || twin_entry_cost<0>(e16, (uint32_t)E) != (int64_t)(-aa) * 4294967296LL + m)
+          return fail(SH_ERR_ARGS, "twin tile entry decode mismatch");
+      }
   }
   DeviceGuard dg(device);  // the caller's device is current again on return
   sh_ctx *ctx = new sh_ctx();
