@@ -3069,6 +3069,13 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
 // and LDS reads up to the relaxation's inputs; B = relaxation, key and argmin;
 // C = winner decode and book-keeping; D = per-Dijkstra set-up, dual update and
 // augmentation.  (s_memtime stamps cost cycles themselves: relative view.)
+// issue-priority steps of santa_sp3_kernel (Dijkstras before the last; see
+// santa_sp2_kernel; -D overrides are for A/B builds only)
+#ifndef SP3_PRIO_A
+#define SP3_PRIO_A 32
+#define SP3_PRIO_B 8
+#define SP3_PRIO_C 2
+#endif
 template <bool TIMED>
 __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const unsigned char *rec_all) {
   // (static LDS: every address below is a constant offset, no base register)
@@ -3165,9 +3172,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
     c4r = (uint32_t)(4 * lane) * 0x01010101u + 0x03020100u;
   } else {
     for (int cur = 0; cur < n; ++cur) {
-      if (cur == n - 32) __builtin_amdgcn_s_setprio(2);  // (santa_sp2_kernel's issue priority)
-      if (cur == n - 8) __builtin_amdgcn_s_setprio(1);
-      if (cur == n - 2) __builtin_amdgcn_s_setprio(0);
+      if (cur == n - SP3_PRIO_A) __builtin_amdgcn_s_setprio(2);  // (santa_sp2_kernel's issue priority)
+      if (cur == n - SP3_PRIO_B) __builtin_amdgcn_s_setprio(1);
+      if (cur == n - SP3_PRIO_C) __builtin_amdgcn_s_setprio(0);
       // Dijkstra set-up: remaining = [n-1 .. 0], every column < n live, spc = inf
       int ln = lane;
       asm volatile("" : "+v"(ln));
