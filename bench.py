@@ -62,8 +62,9 @@ def parse():
                     help="budget per rank count of the reference-semantics baseline B1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--score-check-every", type=int, default=None,
-                    help="0: rescore the whole state every round (the reference); K: the delta "
-                         "all-reduce with a full rescore every K rounds (default: 16 at N > 1, 0 at N = 1)")
+                    help="0: rescore the whole state every round (the reference); K: the round's sums "
+                         "from the block kernels' exact deltas (all-reduced at N > 1) with a full "
+                         "rescore every K rounds that must agree (default 16, every N)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="test only: 'gloo' with --one-device rehearses N ranks on one GPU")
     ap.add_argument("--one-device", action="store_true",

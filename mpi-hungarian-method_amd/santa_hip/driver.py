@@ -138,16 +138,19 @@ class _Sums:
 
     full (check_every == 0): a rescore of the whole state every round, as the
     reference does on every rank (mpi_single.py:157).
-    delta (check_every = K > 0; the default at N > 1): every
+    delta (check_every = K > 0; the default, K = 16): every
     rank's block kernels add the exact happiness deltas of ITS blocks into an
-    int64[2], one all-reduce(sum) of those 16 bytes (RCCL over xGMI) gives the
-    round's delta, and S = S(start state of the round) + delta; a full rescore
-    of the state every K rounds (and after the last round) must agree, or the
-    run stops with an error.  Integer sums: order-free, bit-exact."""
+    int64[2], one all-reduce(sum) of those 16 bytes (RCCL over xGMI; the
+    identity on one rank) gives the round's delta, and S = S(start state of
+    the round) + delta; a full rescore of the state every K rounds (and after
+    the last round) must agree, or the run stops with an error.  Integer
+    sums: order-free, bit-exact -- every round's score equals the full
+    rescore's, at every N (round 3: one GPU also takes its sums from the
+    deltas, 2.5 % per round: profiles/r03_score_mode_ab.jsonl)."""
 
     def __init__(self, engine, world: World, check_every: int | None, max_rounds: int):
         if check_every is None:
-            check_every = 16 if world.distributed else 0
+            check_every = 16
         self.every = int(check_every) if hasattr(engine, "delta_begin") else 0
         self.engine, self.world, self.max_rounds = engine, world, max_rounds
         self.bufs = [engine.new_delta() for _ in range(2)] if self.every else None
@@ -203,7 +206,7 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
     score_check_every: 0 = rescore the whole state every round (the
     reference); K > 0 = the delta all-reduce of SURVEY §8(e) with a full
     rescore every K rounds that must agree (see _Sums); default K = 16 at
-    N > 1 and 0 on one rank.  sums0: the exact (S_child, S_gift) of the
+    every N (same per-round sums either way).  sums0: the exact (S_child, S_gift) of the
     start state, if known (else one rescore)."""
     world = world or World()
     accept = accept or ("always" if mode == _lib.SH_MODE_SINGLE else "improve")

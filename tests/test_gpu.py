@@ -428,11 +428,14 @@ def test_avg_normalized_happiness_api(sh, full_data):
 
 
 # --------------------------------------------------------------------------- driver
+@pytest.mark.parametrize("check", [0, None])
 @pytest.mark.parametrize("mode", ["single", "twins"])
-def test_trajectory_gpu_matches_reference(sh, ctx, full_data, mode, tmp_path):
+def test_trajectory_gpu_matches_reference(sh, ctx, full_data, mode, check, tmp_path):
     """The reference's my_optimizer (3 rounds, P blocks per round) replayed
     on the GPU: scores, states and the per-round checkpoint CSV (byte-
-    identical to the reference's to_csv, mpi_single.py:177) all equal."""
+    identical to the reference's to_csv, mpi_single.py:177) all equal; with
+    the reference's full rescore every round (check = 0, the rescored states'
+    digests compared too) and with the default delta sums (check = None)."""
     import hashlib
 
     from santa_hip import data as D
@@ -455,10 +458,12 @@ def test_trajectory_gpu_matches_reference(sh, ctx, full_data, mode, tmp_path):
 
     m = 0 if mode == "single" else 1
     res = run_rounds(Rec(ctx), types, mode=m, n=g["n"], blocks_per_round=g["P"], seed=g["seed"],
-                     max_rounds=g["rounds"], world=World(), score0=g["score0"], on_round=checkpoint)
+                     max_rounds=g["rounds"], world=World(), score0=g["score0"], on_round=checkpoint,
+                     score_check_every=check)
     assert [st.score for st in res.history] == [r["score"] for r in g["per_round"]]
-    assert shas == [r["types_sha"] for r in g["per_round"]]
     assert csvs == [r["csv"] for r in g["per_round"]]
+    if check == 0:
+        assert shas == [r["types_sha"] for r in g["per_round"]]
 
 
 def test_optimize_block_api(sh, full_data, santa_blocks):
