@@ -312,8 +312,10 @@ def test_bench_rounds_vs_oracle(sh, ctx, full_data, mode, pinned, rounds):
             col = torch.empty(B * n_, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")
             steps = torch.empty(B, dtype=torch.int64, device="cuda")
-            delta = torch.zeros(2, dtype=torch.int64, device="cuda")
-            self.ctx.solve_blocks(mode_, rows_, n_, types_, col=col, cost=cost, delta=delta, steps=steps)
+            dl = torch.zeros(2, dtype=torch.int64, device="cuda")
+            self.ctx.solve_blocks(mode_, rows_, n_, types_, col=col, cost=cost, delta=dl, steps=steps)
+            if delta is not None:  # (the driver's delta sums: this round's blocks too)
+                delta += dl
             t_host = pre.copy()
             r = rows_.cpu().numpy().reshape(B, n_)
             ocol, ocost, osteps = _oracle_round_threaded(mode_, full_data.wish, t_host, r, full_data.ng)
@@ -323,7 +325,7 @@ def test_bench_rounds_vs_oracle(sh, ctx, full_data, mode, pinned, rounds):
             assert int(steps.sum()) == osteps, k
             s0 = oracle.score_sums(full_data.wish, full_data.goodkids, pre)
             s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
-            assert delta.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]], k
+            assert dl.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]], k
             checked.append(k)
 
         def score_sums(self, t):
