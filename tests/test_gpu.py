@@ -823,7 +823,7 @@ def test_two_ranks_on_the_hip_path_equal_one_rank(sh, ctx, full_data, mode, roun
             return s
 
     res = run_rounds(Rec(ctx), types, mode=mode, n=256, seed=41, max_rounds=rounds, patience=100,
-                     world=World())
+                     world=World(), score_check_every=0)  # (the reference: a full rescore every round)
     want = types.cpu().numpy()
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
