@@ -291,24 +291,31 @@ def design_kernels(kname: str):
     return ["santa_tile_kernel", k] if k in ("santa_sp2_kernel", "santa_sp3_kernel") else [k]
 
 
-def stored_occupancy(kname: str):
+def _same_launch(s, blocks):
+    """A summary describes this launch only if its probe ran the same number
+    of blocks per launch (one kernel name covers several workloads: the 4-wave
+    santa_block_kernel runs the twins round and the 8-GPU singles shard)."""
+    return s.get("probe", {}).get("blocks") == blocks
+
+
+def stored_occupancy(kname: str, blocks: int):
     """Mean resident waves per SIMD and LDS-array activity of `kname` from
-    the newest committed PMC summary of THIS kernel source (the "occ" pass of
-    tools/profile_round.sh, round-0 launch), or None."""
+    the newest committed PMC summary of THIS kernel source and launch size
+    (the "occ" pass of tools/profile_round.sh, round-0 launch), or None."""
     src = hashlib.sha256(open(KERNEL_SRC, "rb").read()).hexdigest()[:16]
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
         try:
             s = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if s.get("source_sha16") == src and kname in s.get("occupancy_lds", {}):
+        if s.get("source_sha16") == src and _same_launch(s, blocks) and kname in s.get("occupancy_lds", {}):
             e = dict(s["occupancy_lds"][kname])
             e["source"] = f"{os.path.basename(path)} (round-0 launch, kernel source {src})"
             return e
     return None
 
 
-def stored_traffic(knames):
+def stored_traffic(knames, blocks: int):
     """HBM bytes per launch of the kernels `knames` (summed) from the newest committed rocprofv3 PMC
     summary taken on THIS kernel source (tools/profile_round.sh ->
     profiles/<tag>_summary.json records the source hash).  FETCH_SIZE is
@@ -323,7 +330,7 @@ def stored_traffic(knames):
             s = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if s.get("source_sha16") != src:
+        if s.get("source_sha16") != src or not _same_launch(s, blocks):
             continue
         hb = s.get("hbm_bytes_per_launch", {})
         es = [hb.get(k, {}) for k in knames]
@@ -336,7 +343,8 @@ def stored_traffic(knames):
                                     "fetch_correction": k},
                     "traffic_source": f"{os.path.basename(path)} (kernel source {src})"}
     return {"traffic": None,
-            "traffic_note": f"no committed PMC summary was taken on this kernel source ({src})"}
+            "traffic_note": f"no committed PMC summary was taken on this kernel source ({src}) "
+                            f"at {blocks} blocks per launch"}
 
 
 # --------------------------------------------------------------------------- main
@@ -509,7 +517,7 @@ def main():
             lds = {"bound": "lds", "achieved": round(ach, 3), "peak": round(LDS_PEAK_TBS, 1), "unit": "TB/s",
                    "frac": round(ach / LDS_PEAK_TBS, 4), "bytes_per_step": per_step, "bytes_per_dijkstra": per_dij,
                    "note": "algorithmic LDS bytes of the solve (steps of the timed launches) / kernel time"}
-            occ = stored_occupancy(kshort)
+            occ = stored_occupancy(kshort, my_blocks)
             if occ:
                 lds["pmc"] = occ
         latency = {"steps_per_launch": float(st.sum(axis=1).mean()),
@@ -565,7 +573,7 @@ def main():
         "cpu": cpu,
     }
     if world == 1:  # the PMC passes profile a full one-GPU round (tools/profile_round.sh)
-        out["roofline"].update(stored_traffic(design_kernels(kname)))
+        out["roofline"].update(stored_traffic(design_kernels(kname), my_blocks))
     if cpu_line is not None:
         out["cpu_baseline"] = cpu_line
     if rank == 0:

@@ -1512,13 +1512,14 @@ __host__ __device__ __forceinline__ VtLds vt_lds_layout(int ng) {
   return L;
 }
 
-// SC: the scaled-key solver (sap_solve_mw_sc); a block outside its range, or
-// every block under SH_FLAG_EXACT_ARGMIN / SH_FLAG_TEST_RANGE, is appended to
-// the overflow list untouched and re-solved by the launch of the windowed-key
-// instantiation (SC = false, also the fallback of the register-tile sparse
-// design).  One solver per instantiation: both inlined in one kernel spill
-// the tile.
-template <int MODE, bool SC>
+// SV: the solver, one per instantiation (two inlined in one kernel put the
+// tile in scratch: the row fetch becomes a scratch load per step).
+//   1  lattice 32-bit keys (sap_solve_mw_l32), the production launch;
+//   2  round 2's scaled 64-bit keys (sap_solve_mw_sc), SH_FLAG_SP2 A/B only;
+//   0  windowed keys (sap_solve_mw): the launch over the blocks 1 / 2 left
+//      (outside their range; every block under SH_FLAG_EXACT_ARGMIN /
+//      SH_FLAG_TEST_RANGE), also the fallback of the register-tile sparse design.
+template <int MODE, int SV>
 __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(SantaArgs a) {
   static_assert(MODE == 0, "singles only: VtRegLoader decodes uint8 rank codes");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1673,10 +1674,10 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
   if (a.flags & SH_FLAG_BUILD_ONLY) {
     if (live) c4r_l[j] = (int16_t)j, r4c_l[j] = (int16_t)j;
     __syncthreads();
-  } else if constexpr (SC) {
+  } else if constexpr (SV != 0) {
     bool redo = exact;
     if (!exact) {
-      if (a.flags & SH_FLAG_SP2) {  // (A/B: round 2's 64-bit scaled keys)
+      if constexpr (SV == 2) {  // (A/B: round 2's 64-bit scaled keys)
         const VtRegLoader<SC_SH> ld{nw1, a.E};
         redo = sap_solve_mw_sc<VT_NW>(n, ld, S, steps, (a.flags & SH_FLAG_TEST_RANGE) != 0, T.a, T.b);
       } else {
@@ -4185,11 +4186,11 @@ int launch_santa(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   return SH_OK;
 }
 
-template <int MODE, bool SC = false>
+template <int MODE, int SV = 0>
 int launch_santa_vt(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   const VtLds L = vt_lds_layout(ctx->ng);
   if (L.total > 64 * 1024) return fail(SH_ERR_ARGS, "too many gift types for the LDS chain heads");
-  hipLaunchKernelGGL((santa_vt_kernel<MODE, SC>), dim3(B), dim3(VT_WG), L.total, s, a);
+  hipLaunchKernelGGL((santa_vt_kernel<MODE, SV>), dim3(B), dim3(VT_WG), L.total, s, a);
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
@@ -4276,13 +4277,13 @@ int launch_santa_vt_sc(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   a.ovf_cnt = ctx->d_ovf + p;
   a.ovf_list = ctx->d_ovf + 2 + (size_t)p * ctx->ovf_cap;
   a.blist = nullptr;
-  int rc = launch_santa_vt<0, true>(ctx, a, B, s);
+  int rc = (a.flags & SH_FLAG_SP2) ? launch_santa_vt<0, 2>(ctx, a, B, s) : launch_santa_vt<0, 1>(ctx, a, B, s);
   if (rc == SH_OK) {
     SantaArgs f = a;
     f.blist = a.ovf_list;
     f.bcount = a.ovf_cnt;
     f.ovf_reset = ctx->d_ovf + (p ^ 1);
-    rc = launch_santa_vt<0, false>(ctx, f, B, s);
+    rc = launch_santa_vt<0, 0>(ctx, f, B, s);
   }
   if (rc) {
     (void)hipMemsetAsync(ctx->d_ovf + p, 0, sizeof(int32_t), s);
@@ -4378,7 +4379,7 @@ int lds_tile_slots(sh_ctx *ctx, int n) {
 int vt_tile_slots(sh_ctx *ctx) {
   if (ctx->vt_slots >= 0) return ctx->vt_slots;
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, santa_vt_kernel<0, true>, VT_WG,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, santa_vt_kernel<0, 1>, VT_WG,
                                                    vt_lds_layout(ctx->ng).total) != hipSuccess)
     per_cu = 0;
   ctx->vt_slots = per_cu * ctx->n_cu;

@@ -8,6 +8,7 @@
   reference's arithmetic (mpi_single.py:238-240, mpi_twins.py:244-246).
 """
 import ctypes
+import json
 import os
 import re
 
@@ -215,7 +216,9 @@ def test_bench_roofline_helpers():
     """bench.py's roofline plumbing on the CPU: the register-tile design's
     launch is two kernels (tile build + solve), and the stored HBM traffic
     comes only from a committed rocprofv3 summary of the same kernel source
-    (otherwise null with a note naming the source hash)."""
+    and launch size (otherwise null with a note naming the source hash); one
+    kernel name that serves two launch sizes (the 4-wave kernel: the twins
+    round and the 8-GPU shard) never borrows the other size's figures."""
     import importlib.util
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -225,7 +228,17 @@ def test_bench_roofline_helpers():
     assert bench.design_kernels("santa_sp2_kernel (1-wave sparse register tile)") == \
         ["santa_tile_kernel", "santa_sp2_kernel"]
     assert bench.design_kernels("santa_block_kernel (twins, 4-wave code-pair tile)") == ["santa_block_kernel"]
-    t = bench.stored_traffic(["santa_tile_kernel", "santa_sp2_kernel"])
+    for blocks in (78, 466, 467, 12345):
+        t = bench.stored_traffic(["santa_block_kernel"], blocks)
+        if t["traffic"] is not None:
+            s = json.load(open(os.path.join(root, "profiles", t["traffic_source"].split(" ")[0])))
+            assert s["probe"]["blocks"] == blocks
+        o = bench.stored_occupancy("santa_block_kernel", blocks)
+        if o is not None:
+            s = json.load(open(os.path.join(root, "profiles", o["source"].split(" ")[0])))
+            assert s["probe"]["blocks"] == blocks
+    assert bench.stored_traffic(["santa_block_kernel"], 12345)["traffic"] is None
+    t = bench.stored_traffic(["santa_tile_kernel", "santa_sp2_kernel"], 3730)
     if t["traffic"] is None:
         assert "kernel source" in t["traffic_note"]
     else:

@@ -22,6 +22,25 @@ def pmc(path):
     return agg
 
 
+def by_short(agg, main=None):
+    """Merge the instantiations of one kernel (e.g. santa_vt_kernel<0, true>
+    and its fallback launch santa_vt_kernel<0, false>) under the short name:
+    counters summed (HBM bytes of the whole solve), or, with `main`, the
+    instantiation with the largest `main` counter kept (the launch that did
+    the work, for per-wave and occupancy figures)."""
+    out = {}
+    for k, v in agg.items():
+        s = short(k)
+        if s not in out:
+            out[s] = dict(v)
+        elif main is None:
+            for c, x in v.items():
+                out[s][c] = out[s].get(c, 0.0) + x
+        elif v.get(main, 0.0) > out[s].get(main, 0.0):
+            out[s] = dict(v)
+    return out
+
+
 def short(name):
     for key in ("santa_sp3_kernel", "santa_sp2_kernel", "santa_tile_kernel", "santa_sp_kernel", "santa_vt_kernel", "santa_sw_kernel", "santa_block_kernel",
                 "santa_big_kernel", "score_kernel",
@@ -72,8 +91,8 @@ def main(src, tag, root):
     fscore = pmc(os.path.join(src, "fetch_score_counter_collection.csv"))
     hbm = {}
     for d, key in ((fetch, "FETCH_SIZE"), (write, "WRITE_SIZE"), (fscore, "FETCH_SIZE")):
-        for k, v in d.items():
-            hbm.setdefault(short(k), {})[key + "_bytes"] = v.get(key, 0.0) * 1024
+        for k, v in by_short(d).items():
+            hbm.setdefault(k, {})[key + "_bytes"] = v.get(key, 0.0) * 1024
     out["hbm_bytes_per_launch"] = hbm
     probe = {}
     pj = os.path.join(src, "probe_sq1.json")
@@ -84,14 +103,14 @@ def main(src, tag, root):
         sq[k].update(v)
     steps = probe.get("steps_total")
     sqs = {}
-    for k, v in sq.items():
+    for k, v in by_short(sq, "SQ_WAVE_CYCLES").items():
         waves = v.get("SQ_WAVES", 0) or 1
         e = {c: x for c, x in v.items()}
         if steps:
             wps = steps * waves / probe["blocks"]
             e["per_wave_step_quadcycles"] = {c: x / wps for c, x in v.items() if c.startswith("SQ_")
                                              and c != "SQ_WAVES"}
-        sqs[short(k)] = e
+        sqs[k] = e
     out["sq"] = sqs
     out["probe"] = probe
     # occupancy and LDS activity (own PMC pass, tools/profile_round.sh "occ"):
@@ -102,7 +121,7 @@ def main(src, tag, root):
     #   conflict share = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE.
     n_cu = 256
     occ = {}
-    for k, v in pmc(os.path.join(src, "occ_counter_collection.csv")).items():
+    for k, v in by_short(pmc(os.path.join(src, "occ_counter_collection.csv")), "GRBM_GUI_ACTIVE").items():
         grbm = v.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
         if not grbm:
             continue
@@ -112,7 +131,7 @@ def main(src, tag, root):
             e["lds_array_busy_frac"] = v["SQ_LDS_IDX_ACTIVE"] / (grbm * n_cu)
             e["lds_bank_conflict_frac"] = v.get("SQ_LDS_BANK_CONFLICT", 0.0) / v["SQ_LDS_IDX_ACTIVE"]
             e["lds_insts"] = v.get("SQ_INSTS_LDS", 0.0)
-        occ[short(k)] = e
+        occ[k] = e
     if occ:
         out["occupancy_lds"] = occ
     po = os.path.join(src, "probe_occ.json")
