@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-end evidence on the current source (GPU box), in two calls:
-#   phase 1: the GPU test suite, smoke(), rocprofv3 profiles (tag $TAG, $TAG"t" for twins);
+#   phase 1: the GPU test suite, smoke(), rocprofv3 profiles (tag $TAG, $TAG"t" for twins,
+#            $TAG"s8/s4/s2" for rank 0's shard at N = 8, 4, 2);
 #            then locally: python tools/summarize_profile.py gpurun_out/prof_<tag> <tag>
 #   phase 2: bench lines for every mode (they read the committed summaries), shard probes
 cd "$(dirname "$0")/.." || exit 2
@@ -11,6 +12,7 @@ case ${1:-1} in
     grep -q " passed" gpurun_out/tests.log && ! grep -q " failed" gpurun_out/tests.log || exit 1
     bash tools/profile_round.sh $TAG single > gpurun_out/prof_$TAG.log 2>&1 || exit 1
     bash tools/profile_round.sh ${TAG}t twins > gpurun_out/prof_${TAG}t.log 2>&1 || exit 1
+    bash tools/profile_shards.sh ${TAG}s || exit 1
     ;;
   2)
     bash tools/gpu_run.sh bench bench_twins bench_triplets bench_n2000 > gpurun_out/final_bench.log 2>&1 || exit 1
