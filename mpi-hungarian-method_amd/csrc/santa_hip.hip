@@ -2469,20 +2469,36 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
   u32x32 G0, G1;
   {
     const int16_t *src = a.wish + (size_t)child * nw;
-    if constexpr (VEC) {  // n_wish % 4 == 0: 8-byte chunks
-      const uint2 *s2 = (const uint2 *)src;
-      const int nch = nw >> 2;
+    if constexpr (VEC) {  // n_wish % 4 == 0: rows are 8-byte aligned
+      // 16-byte loads of the 16-byte aligned window around the row, then a
+      // per-lane shift by two dwords when the row starts at 8 mod 16.  One
+      // row per lane means a distinct line per lane and load: the launch is
+      // bound by the texture path's per-instruction address work (TA busy
+      // 73 % of the kernel, profiles/r03_ta_probe.json), so half the load
+      // instructions of 8-byte chunks.  Words past the row are never read
+      // (the passes stop at ndw); the last child's window reads up to 8 bytes
+      // past the array, inside the 16 bytes of padding sh_ctx_create allocates.
+      const bool odd = ((uintptr_t)src & 8u) != 0;
+      const uint4 *s4 = (const uint4 *)(src - (odd ? 4 : 0));  // (pointer arithmetic: stays global)
+      const int nq = (2 * nw + 8 + 15) >> 4;  // window chunks (<= 17 for n_wish <= 128)
+      uint32_t Wd[68];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const uint2 v = (live && c < nch) ? s2[c] : make_uint2(0, 0);
-        G0[2 * c] = v.x;
-        G0[2 * c + 1] = v.y;
+      for (int c = 0; c < 17; ++c) {
+        const uint4 v = (live && c < nq) ? s4[c] : make_uint4(0, 0, 0, 0);
+        Wd[4 * c] = v.x;
+        Wd[4 * c + 1] = v.y;
+        Wd[4 * c + 2] = v.z;
+        Wd[4 * c + 3] = v.w;
       }
+      const uint32_t om = odd ? ~0u : 0u;  // (a mask select: an odd ? Wd[d + 2] : Wd[d] became
+                                           //  an indexed read of Wd in scratch)
 #pragma unroll
-      for (int c = 16; c < 32; ++c) {
-        const uint2 v = (live && c < nch) ? s2[c] : make_uint2(0, 0);
-        G1[2 * c - 32] = v.x;
-        G1[2 * c - 31] = v.y;
+      for (int d = 0; d < 64; ++d) {
+        const uint32_t x = (Wd[d] & ~om) | (Wd[d + 2] & om);
+        if (d < 32)
+          G0[d] = x;
+        else
+          G1[d - 32] = x;
       }
     } else {
 #pragma unroll
