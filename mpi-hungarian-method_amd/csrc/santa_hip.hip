@@ -1072,6 +1072,7 @@ struct SantaArgs {
   int64_t *delta;         // [2] nullable
   int64_t *steps;         // [B] nullable
   const int16_t *wish;    // [nc * n_wish]
+  const uint32_t *wish10;  // [nc * 32] or null: each row's gift ids packed 10 bits apart (128 B rows)
   const int32_t *csr_off; // [nc + 1]
   const uint32_t *csr;    // gift << 16 | rank
   int32_t *err;           // [0] error flags, [1] exact-argmin fallback steps
@@ -2431,8 +2432,14 @@ __host__ __device__ __forceinline__ TileLds tile_lds_layout(int ng) {
 // transposed into the record's VGPR layout with coalesced 16-byte stores.
 // (Round 2's first version built 8 rows per sub-round with 8 lanes per row
 // and a wave scan: ~8,500 instructions per wave against ~3,000 here.)
-template <bool VEC>
+// LV: how a lane loads its row's wishlist -- 0: 2-byte gifts (any n_wish);
+// 1: 16-byte loads of the window around the 8-byte aligned row (n_wish % 4 ==
+// 0); 2: the context's packed copy, 10 bits per gift in one 128-byte line
+// per row (n_wish % 4 == 0, n_wish <= 102, ng <= 1024): 8 aligned 16-byte
+// loads touching one line.
+template <int LV>
 __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(4))) void santa_tile_kernel(SantaArgs a, unsigned char *rec_all) {
+  constexpr bool VEC = LV != 0;  // (n_wish % 4 == 0: no per-gift bound test)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2469,7 +2476,19 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
   u32x32 G0, G1;
   {
     const int16_t *src = a.wish + (size_t)child * nw;
-    if constexpr (VEC) {  // n_wish % 4 == 0: rows are 8-byte aligned
+    if constexpr (LV == 2) {
+      const uint4 *s4 = (const uint4 *)(a.wish10 + (size_t)child * 32);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint4 v = live ? s4[c] : make_uint4(0, 0, 0, 0);
+        G0[4 * c] = v.x;
+        G0[4 * c + 1] = v.y;
+        G0[4 * c + 2] = v.z;
+        G0[4 * c + 3] = v.w;
+      }
+#pragma unroll
+      for (int d = 0; d < 32; ++d) G1[d] = 0;
+    } else if constexpr (LV == 1) {  // n_wish % 4 == 0: rows are 8-byte aligned
       // 16-byte loads of the 16-byte aligned window around the row, then a
       // per-lane shift by two dwords when the row starts at 8 mod 16.  One
       // row per lane means a distinct line per lane and load: the launch is
@@ -2565,6 +2584,17 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
   // (gifts four at a time: dwords d, d + 1 of the register copy, four type-table
   // reads in flight; r >= n_wish pads read type 0 and are masked out)
   auto gifts4 = [&](int d, int (&g)[4]) {
+    if constexpr (LV == 2) {  // gifts 2d .. 2d + 3: bits 20d .. 20d + 39 of the packed row
+      const int bit = 20 * d, dw = bit >> 5, sh = bit & 31;
+      const uint32_t w0 = G0[dw & 31], w1 = G0[(dw + 1) & 31], w2 = G0[(dw + 2) & 31];
+      const uint32_t x = __builtin_amdgcn_alignbit(w1, w0, sh);
+      const uint32_t y = __builtin_amdgcn_alignbit(w2, w1, sh);
+      g[0] = (int)(x & 1023u);
+      g[1] = (int)((x >> 10) & 1023u);
+      g[2] = (int)((x >> 20) & 1023u);
+      g[3] = (int)(__builtin_amdgcn_alignbit(y, x, 30) & 1023u);
+      return;
+    }
     const uint32_t w0 = (d < 32) ? G0[d] : G1[d - 32];
     const uint32_t w1 = (d + 1 < 32) ? G0[d + 1] : G1[d - 31];
     g[0] = (int)(w0 & 0xFFFFu);
@@ -3999,6 +4029,7 @@ struct sh_ctx {
   int nc, ng, nq, n_wish, n_good;
   int64_t E;
   int16_t *d_wish = nullptr;
+  uint32_t *d_wish10 = nullptr;  // packed copy for the tile build (santa_tile_kernel<2>), or null
   int32_t *d_csr_off = nullptr;
   uint32_t *d_csr = nullptr;
   int32_t *d_err = nullptr;
@@ -4131,6 +4162,24 @@ int sh_ctx_create(sh_ctx **out, int device, const int16_t *h_wish, int n_wish,
       (ent.size() && (e = hipMemcpy(ctx->d_csr, ent.data(), ent.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) ||
       (e = hipMemset(ctx->d_err, 0, 16)) != hipSuccess)
     return cleanup(fail(SH_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)));
+  // the tile build's packed wishlist: gift r of a row at bits 10 r .. 10 r + 9
+  // of its 32-dword line (one 128-byte line per row instead of 200 bytes over
+  // two or three)
+  if (n_wish % 4 == 0 && n_wish <= 102 && ng <= 1024) {
+    std::vector<uint32_t> pk((size_t)nc * 32, 0u);
+    for (int c = 0; c < nc; ++c) {
+      const int16_t *row = h_wish + (size_t)c * n_wish;
+      uint32_t *dst = pk.data() + (size_t)c * 32;
+      for (int r = 0; r < n_wish; ++r) {
+        const uint32_t g = (uint32_t)row[r], bit = 10u * (uint32_t)r, sh = bit & 31u;
+        dst[bit >> 5] |= g << sh;
+        if (sh > 22u) dst[(bit >> 5) + 1] |= g >> (32u - sh);
+      }
+    }
+    if ((e = hipMalloc(&ctx->d_wish10, pk.size() * 4)) != hipSuccess ||
+        (e = hipMemcpy(ctx->d_wish10, pk.data(), pk.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+      return cleanup(fail(SH_ERR_HIP, std::string("packed wishlist: ") + hipGetErrorString(e)));
+  }
   int lds = 0;
   if ((e = hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device)) != hipSuccess)
     return cleanup(fail(SH_ERR_HIP, hipGetErrorString(e)));
@@ -4145,6 +4194,7 @@ void sh_ctx_destroy(sh_ctx *ctx) {
   if (!ctx) return;
   DeviceGuard dg(ctx->device);
   if (ctx->d_wish) (void)hipFree(ctx->d_wish);
+  if (ctx->d_wish10) (void)hipFree(ctx->d_wish10);
   if (ctx->d_csr_off) (void)hipFree(ctx->d_csr_off);
   if (ctx->d_csr) (void)hipFree(ctx->d_csr);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
@@ -4335,10 +4385,12 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
     // overflow capacity per block; a sparse budget set for tests lowers it
     // (budget / 16 entries) so that some or all blocks take the fallback
     a.cap = ctx->sp_budget > 0 ? std::min(SP2_OVF_CAP, ctx->sp_budget / 16) : SP2_OVF_CAP;
-    if (vec)
-      hipLaunchKernelGGL(santa_tile_kernel<true>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
+    if (ctx->d_wish10)
+      hipLaunchKernelGGL(santa_tile_kernel<2>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
+    else if (vec)
+      hipLaunchKernelGGL(santa_tile_kernel<1>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
     else
-      hipLaunchKernelGGL(santa_tile_kernel<false>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
+      hipLaunchKernelGGL(santa_tile_kernel<0>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
     HIP_TRY(hipGetLastError());
     if (a.flags & SH_FLAG_EXACT_ARGMIN)
       hipLaunchKernelGGL(santa_sp2_kernel<true>, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
@@ -4485,7 +4537,7 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   DeviceGuard dg(ctx->device);
   SantaArgs a;
   a.rows = d_rows; a.types = d_types; a.col = d_col; a.cost = d_cost; a.delta = d_delta;
-  a.steps = d_steps; a.wish = ctx->d_wish; a.csr_off = ctx->d_csr_off; a.csr = ctx->d_csr;
+  a.steps = d_steps; a.wish = ctx->d_wish; a.wish10 = ctx->d_wish10; a.csr_off = ctx->d_csr_off; a.csr = ctx->d_csr;
   a.err = ctx->d_err; a.E = ctx->E; a.n = n; a.nc = ctx->nc; a.ng = ctx->ng;
   a.n_wish = ctx->n_wish; a.n_good = ctx->n_good; a.flags = flags;
   a.cap = 0; a.ovf_cnt = nullptr; a.ovf_list = nullptr;

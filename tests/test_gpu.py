@@ -982,10 +982,13 @@ def test_no_apply_solves_overlapping_blocks(sh, ctx, full_data):
     assert ctx.error_flags() == 0
 
 
-@pytest.mark.parametrize("nw,ng,nq", [(10, 300, 100), (7, 200, 150), (10, 80, 375), (12, 100, 300)])
+@pytest.mark.parametrize("nw,ng,nq", [(10, 300, 100), (7, 200, 150), (10, 80, 375), (12, 100, 300),
+                                      (104, 200, 100), (100, 120, 200)])
 def test_small_wishlists_match_oracle(sh, nw, ng, nq):
-    """Wishlists whose length is not a multiple of 4 (the tile build's generic
-    load path), odd lengths, and few gift types (types with 4+ columns in a
+    """The tile build's three wishlist loads: lengths that are not a multiple
+    of 4 and odd lengths (2-byte gifts), n_wish = 104 (16-byte windows of the
+    8-byte aligned rows), n_wish = 12 and 100 (the context's 10-bit packed
+    rows); few gift types (types with 4+ columns in a
     block: the column-sort spill list; rows with more than 32 hits: the
     overflow list and, past its capacity, the fallback launch): the sparse
     design and the LDS-tile kernel equal the oracle's round bit for bit."""
