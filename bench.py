@@ -318,11 +318,12 @@ def stored_occupancy(kname: str, blocks: int):
 def stored_traffic(knames, blocks: int):
     """HBM bytes per launch of the kernels `knames` (summed) from the newest committed rocprofv3 PMC
     summary taken on THIS kernel source (tools/profile_round.sh ->
-    profiles/<tag>_summary.json records the source hash).  FETCH_SIZE is
-    scaled by the factor calibrated for this kernel's access pattern (random
-    200-byte wishlist rows, 8-byte lane loads; the guide's 2x rule holds only
-    for 16 B/lane streams: tools/calib/gather_calib.hip,
-    profiles/<tag>_fetch_calibration.json); WRITE_SIZE is taken as read."""
+    profiles/<tag>_summary.json records the source hash).  Each kernel's
+    FETCH_SIZE is scaled by the factor calibrated for its access pattern
+    (tools/calib/gather_calib.hip, profiles/<tag>_fetch_calibration.json:
+    kernel_factors -- the tile build's one-line packed rows, the solve's
+    16 B/lane record stream -- else the 8-byte row-gather factor); WRITE_SIZE
+    is taken as read."""
     src = hashlib.sha256(open(KERNEL_SRC, "rb").read()).hexdigest()[:16]
     calib = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fetch_calibration.json")))
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True):
@@ -335,12 +336,15 @@ def stored_traffic(knames, blocks: int):
         hb = s.get("hbm_bytes_per_launch", {})
         es = [hb.get(k, {}) for k in knames]
         if all("FETCH_SIZE_bytes" in e and "WRITE_SIZE_bytes" in e for e in es):
-            k = json.load(open(calib[-1]))["gather_correction_factor"] if calib else 1.0
+            cal = json.load(open(calib[-1])) if calib else {}
+            ks = [cal.get("kernel_factors", {}).get(kn, cal.get("gather_correction_factor", 1.0)) for kn in knames]
             fetch = sum(e["FETCH_SIZE_bytes"] for e in es)
             write = sum(e["WRITE_SIZE_bytes"] for e in es)
-            return {"traffic": round(fetch * k + write),
+            est = sum(e["FETCH_SIZE_bytes"] * k for e, k in zip(es, ks)) + write
+            return {"traffic": round(est),
                     "traffic_raw": {"FETCH_SIZE": fetch, "WRITE_SIZE": write, "kernels": knames,
-                                    "fetch_correction": k},
+                                    "fetch_correction": ks,
+                                    "calibration": os.path.basename(calib[-1]) if calib else None},
                     "traffic_source": f"{os.path.basename(path)} (kernel source {src})"}
     return {"traffic": None,
             "traffic_note": f"no committed PMC summary was taken on this kernel source ({src}) "

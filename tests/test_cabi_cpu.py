@@ -243,5 +243,8 @@ def test_bench_roofline_helpers():
         assert "kernel source" in t["traffic_note"]
     else:
         raw = t["traffic_raw"]
-        assert t["traffic"] == round(raw["FETCH_SIZE"] * raw["fetch_correction"] + raw["WRITE_SIZE"])
+        s = json.load(open(os.path.join(root, "profiles", t["traffic_source"].split(" ")[0])))
+        hb = s["hbm_bytes_per_launch"]
+        est = sum(hb[k]["FETCH_SIZE_bytes"] * f for k, f in zip(raw["kernels"], raw["fetch_correction"]))
+        assert t["traffic"] == round(est + raw["WRITE_SIZE"])
         assert raw["kernels"] == ["santa_tile_kernel", "santa_sp2_kernel"]

@@ -9,7 +9,9 @@
 // prints the number of distinct 128-byte lines it touches; FETCH_SIZE (x1024)
 // of the `gather_rows` dispatch divided by lines x 128 is the correction
 // factor for this pattern.  A second kernel streams the table with 16 B per
-// lane (the guide's calibrated case) as a control.
+// lane (the guide's calibrated case) as a control.  A third (round 3e)
+// repeats the tile build's packed-wishlist pattern: one lane per random
+// 128-byte aligned row of a 1M x 128 B table, 8 x 16-byte loads (one line).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -39,6 +41,20 @@ __global__ void gather_rows(const uint8_t *tab, const int32_t *rows, int R, uint
     for (int c = 0; c < 4; ++c) {
       const int o = (c * 8 + q) * 8;  // chunk (c*8+q) of 25
       if (o < ROW) acc += *(const uint64_t *)(p + o);
+    }
+  }
+  if (acc == 0x0123456789ABCDEFull) sink[0] = acc;  // keep the loads
+}
+
+__global__ void gather_lines(const uint4 *tab, const int32_t *rows, int R, uint64_t *sink) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t acc = 0;
+  if (r < R) {
+    const uint4 *p = tab + (size_t)rows[r] * 8;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {  // (64-bit terms: a 32-bit sum could never reach the sink test)
+      const uint4 v = p[c];
+      acc = acc * 31u + ((((uint64_t)v.x << 32) | v.y) ^ (((uint64_t)v.z << 32) | v.w));
     }
   }
   if (acc == 0x0123456789ABCDEFull) sink[0] = acc;  // keep the loads
@@ -92,9 +108,19 @@ int main() {
   CK(hipDeviceSynchronize());
   hipLaunchKernelGGL(stream16, dim3(4096), dim3(256), 0, 0, (const uint4 *)tab, (size_t)NC * ROW / 16, sink);
   CK(hipDeviceSynchronize());
+  // packed-row gather: R distinct random 128-byte lines, one lane each
+  uint4 *tab128;
+  CK(hipMalloc(&tab128, (size_t)NC * 128));
+  CK(hipMemset(tab128, 3, (size_t)NC * 128));
+  CK(hipDeviceSynchronize());
+  hipLaunchKernelGGL(stream16, dim3(4096), dim3(256), 0, 0, (const uint4 *)flush, FL / 16, sink);
+  CK(hipDeviceSynchronize());
+  hipLaunchKernelGGL(gather_lines, dim3((R + threads - 1) / threads), dim3(threads), 0, 0, tab128, rows, R, sink);
+  CK(hipDeviceSynchronize());
   printf("{\"rows\": %d, \"row_bytes\": %d, \"distinct_lines_128\": %zu, \"line_bytes\": %zu, "
-         "\"useful_bytes\": %zu, \"stream16_bytes\": %zu, \"flush_bytes\": %zu}\n",
-         R, ROW, lines, lines * 128, (size_t)R * ROW, (size_t)NC * ROW, FL);
+         "\"useful_bytes\": %zu, \"stream16_bytes\": %zu, \"flush_bytes\": %zu, \"packed_line_bytes\": %zu}\n",
+         R, ROW, lines, lines * 128, (size_t)R * ROW, (size_t)NC * ROW, FL, (size_t)R * 128);
+  CK(hipFree(tab128));
   CK(hipFree(flush));
   CK(hipFree(tab));
   CK(hipFree(rows));
