@@ -110,7 +110,10 @@ int sh_version(void);
  * good-kids CSVs, the 4 GB dense child_happiness table and gift_ids).  The
  * dense table is never materialised: cost tiles are rebuilt per block from the
  * wishlist rows.  Also builds the child -> (gift, rank) inverse of the
- * good-kids lists used by the score.
+ * good-kids lists used by the score, and (n_wish % 4 == 0, n_wish <= 102,
+ * ng <= 1024: the Kaggle shape) a second device copy of the wishlists packed
+ * 10 bits per gift in one 128-byte line per child for the tile build
+ * (nc x 128 bytes: 128 MB for 1M children, beside the 200 MB int16 copy).
  *   h_wish     int16 [nc x n_wish]  child_wishlist (column 0 = ChildId dropped)
  *   h_goodkids int32 [ng x n_good]  gift_goodkids  (column 0 = GiftId dropped)
  *   nq         units per gift type (1000; the Kaggle data has nc == ng * nq,
