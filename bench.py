@@ -38,10 +38,9 @@ LDS_PEAK_TBS = 256 * 256 * 2.4e9 / 1e12
 # Algorithmic LDS bytes of the solve per Dijkstra step and per Dijkstra (all
 # lanes of the block's waves): santa_sp3_kernel per step =
 # 64 lanes x (4 scatter + 16 row read + 4 un-scatter + 4 u + 1 + 1 remaining),
-# per Dijkstra 64 x (4 remaining + 16 dual atomics); santa_sp2_kernel the
-# same with 8-byte costs and duals; the 4-wave kernels per step = 256 threads
+# per Dijkstra 64 x (4 remaining + 16 dual atomics); the 4-wave kernels per step = 256 threads
 # x (1 tile byte + 4 u + 8 step word) + the fold, per Dijkstra 256 x 12.
-LDS_BYTES = {"santa_sp3_kernel": (64 * 30, 64 * 20), "santa_sp2_kernel": (64 * 58, 64 * 36),
+LDS_BYTES = {"santa_sp3_kernel": (64 * 30, 64 * 20),
              "santa_block_kernel": (256 * 13, 256 * 12), "santa_vt_kernel": (256 * 12, 256 * 12)}
 CLOCK_HZ = 2.4e9               # MI355X max shader clock (MI355X_MICROARCH.md)
 KERNEL_SRC = os.path.join(ROOT, "mpi-hungarian-method_amd", "csrc", "santa_hip.hip")
@@ -288,7 +287,7 @@ def design_kernels(kname: str):
     design builds its tiles in santa_tile_kernel, then solves in santa_sp3_kernel;
     the events around the solve bracket both)."""
     k = kname.split(" ")[0].split("<")[0]
-    return ["santa_tile_kernel", k] if k in ("santa_sp2_kernel", "santa_sp3_kernel") else [k]
+    return ["santa_tile_kernel", k] if k == "santa_sp3_kernel" else [k]
 
 
 def _same_launch(s, blocks):
@@ -493,8 +492,7 @@ def main():
         bmax = int(st[0].argmax())
         rows0 = ctx.sample_blocks(mode, n, nb, args.seed, 0)
         one = rows0[(b0 + bmax) * n:(b0 + bmax + 1) * n].contiguous()
-        force = {0: _lib.SH_FLAG_SP_TILE, 6: _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_SP2, 7: _lib.SH_FLAG_SP_TILE,
-                 1: _lib.SH_FLAG_LDS_TILE}.get(design, 0)
+        force = {0: _lib.SH_FLAG_SP_TILE, 7: _lib.SH_FLAG_SP_TILE, 1: _lib.SH_FLAG_LDS_TILE}.get(design, 0)
         lone = []
         for _ in range(3):
             tt = ctx.upload_types(sd.types)
@@ -576,8 +574,10 @@ def main():
                      "algorithmic_bytes_per_block": per_block, "latency": latency, "lds": lds},
         "cpu": cpu,
     }
-    if world == 1:  # the PMC passes profile a full one-GPU round (tools/profile_round.sh)
-        out["roofline"].update(stored_traffic(design_kernels(kname), my_blocks))
+    # PMC summaries of the same kernel source and launch size: the full one-GPU
+    # round (tools/profile_round.sh) or rank 0's shard at N = 2, 4, 8
+    # (tools/profile_shards.sh); else a traffic_note says none was taken
+    out["roofline"].update(stored_traffic(design_kernels(kname), my_blocks))
     if cpu_line is not None:
         out["cpu_baseline"] = cpu_line
     if rank == 0:

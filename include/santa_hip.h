@@ -69,10 +69,10 @@ extern "C" {
                                    treats every block as outside its
                                    scaled-unit range, so all blocks take the
                                    fallback launch (same results)          */
-#define SH_FLAG_SP2 2048u      /* force the 64-bit-key one-wave register-tile
-                                   solver (santa_sp2_kernel, round 2's
-                                   default) instead of santa_sp3_kernel (A/B;
-                                   identical results)                      */
+#define SH_FLAG_SP2 2048u      /* RETIRED (round 4): round 2's 64-bit-key
+                                   one-wave kernel (santa_sp2_kernel) left
+                                   the library; every entry point returns
+                                   SH_ERR_ARGS for this flag               */
 #define SH_FLAG_NO_APPLY 1024u  /* solve and report (col, cost, deltas,
                                    steps) but leave the gift types untouched:
                                    blocks may then overlap (batched
@@ -85,9 +85,9 @@ extern "C" {
 #define SH_DESIGN_VT_TILE 3  /* 4 waves, register tile (one resident wave) */
 #define SH_DESIGN_TWINS 4    /* twins n <= 256: 4 waves, code-pair tile     */
 #define SH_DESIGN_LARGE 5    /* n > 256: row rebuilt from the wishlist      */
-#define SH_DESIGN_SPARSE2 6  /* one wave per block, hit tile in VGPRs,
-                                64-bit keys (SH_FLAG_SP2)                   */
-#define SH_DESIGN_SPARSE3 7  /* as 6 with 32-bit lattice keys (default)     */
+#define SH_DESIGN_SPARSE2 6  /* retired (never returned)                    */
+#define SH_DESIGN_SPARSE3 7  /* one wave per block, hit tile in VGPRs,
+                                32-bit lattice keys (full rounds, default)  */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024

@@ -1279,13 +1279,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
     if (!exact) {
       const bool force = (a.flags & SH_FLAG_TEST_RANGE) != 0;
       if constexpr (MODE == 0) {
-        if (a.flags & SH_FLAG_SP2) {  // (A/B: round 2's 64-bit scaled keys)
-          const TileU8Loader<SANTA_NW, 1, SC_SH> ld{tile8, RS, nw1, a.E};
-          redo = sap_solve_mw_sc<SANTA_NW>(n, ld, S, steps, force);
-        } else {
-          const TileU8LoaderV ld{tile8, RS, nw1};
-          redo = sap_solve_mw_l32<SANTA_NW, TIMED>(n, ld, S, steps, force, a.E, seg);
-        }
+        const TileU8LoaderV ld{tile8, RS, nw1};
+        redo = sap_solve_mw_l32<SANTA_NW, TIMED>(n, ld, S, steps, force, a.E, seg);
       } else {
         const TileU16Loader<SANTA_NW, 1, SC_SH> ld{(const uint16_t *)tile8, E32, RS};
         redo = sap_solve_mw_sc<SANTA_NW>(n, ld, S, steps, force);
@@ -1516,21 +1511,13 @@ __host__ __device__ __forceinline__ VtLds vt_lds_layout(int ng) {
 // SV: the solver, one per instantiation (two inlined in one kernel put the
 // tile in scratch: the row fetch becomes a scratch load per step).
 //   1  lattice 32-bit keys (sap_solve_mw_l32), the production launch;
-//   2  round 2's scaled 64-bit keys (sap_solve_mw_sc), SH_FLAG_SP2 A/B only;
-//   0  windowed keys (sap_solve_mw): the launch over the blocks 1 / 2 left
+//   0  windowed keys (sap_solve_mw): the launch over the blocks 1 left
 //      (outside their range; every block under SH_FLAG_EXACT_ARGMIN /
 //      SH_FLAG_TEST_RANGE), also the fallback of the register-tile sparse design.
 template <int MODE, int SV>
-__global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(SantaArgs a) {
-  static_assert(MODE == 0, "singles only: VtRegLoader decodes uint8 rank codes");
+__device__ __forceinline__ void santa_vt_block(const SantaArgs &a, const int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (a.blist) {  // fallback launch: solve only the listed blocks
-    if (b == 0 && tid == 0) *a.ovf_reset = 0;
-    if (b >= *a.bcount) return;
-    b = a.blist[b];
-  }
   const int n = a.n;
   const VtLds L = vt_lds_layout(a.ng);
   uint8_t *stage = smem + L.stage;
@@ -1678,14 +1665,9 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
   } else if constexpr (SV != 0) {
     bool redo = exact;
     if (!exact) {
-      if constexpr (SV == 2) {  // (A/B: round 2's 64-bit scaled keys)
-        const VtRegLoader<SC_SH> ld{nw1, a.E};
-        redo = sap_solve_mw_sc<VT_NW>(n, ld, S, steps, (a.flags & SH_FLAG_TEST_RANGE) != 0, T.a, T.b);
-      } else {
-        const VtRegLoaderV ld{nw1};
-        redo = sap_solve_mw_l32<VT_NW>(n, ld, S, steps, (a.flags & SH_FLAG_TEST_RANGE) != 0, a.E, nullptr,
-                                       T.a, T.b);
-      }
+      const VtRegLoaderV ld{nw1};
+      redo = sap_solve_mw_l32<VT_NW>(n, ld, S, steps, (a.flags & SH_FLAG_TEST_RANGE) != 0, a.E, nullptr,
+                                     T.a, T.b);
     }
     if (redo) {  // (block-uniform) left untouched for the windowed-key launch
       if (tid == 0) {
@@ -1761,6 +1743,29 @@ __global__ __launch_bounds__(VT_WG, MODE == 0 ? 4 : 2) void santa_vt_kernel(Sant
       atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)td1);
     }
     if (fallbacks) atomicAdd(a.err + 1, fallbacks);
+  }
+}
+
+// SV = 1 (the 4-wave register-tile design's launch): one workgroup per block.
+// SV = 0 is only ever the fallback launch (a.blist: the blocks another launch
+// left, count *a.bcount, usually 0): a small grid that loops over the list,
+// so an empty list costs one workgroup per CU that exits at once instead of
+// one per block of the round (26 x 4.4 us per bench).
+// The loop raises its register demand past the 4-waves-per-SIMD budget (the
+// register tile went to scratch), so the fallback kernel is built for one
+// wave per SIMD: it rarely has work, and never much.
+template <int MODE, int SV>
+__global__ __launch_bounds__(VT_WG, SV == 0 ? 1 : 4) void santa_vt_kernel(SantaArgs a) {
+  static_assert(MODE == 0, "singles only: VtRegLoader decodes uint8 rank codes");
+  if constexpr (SV == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.ovf_reset = 0;
+    const int cnt = *a.bcount;
+    for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
+      santa_vt_block<MODE, SV>(a, a.blist[q]);
+      __syncthreads();  // (LDS reused by the next listed block)
+    }
+  } else {
+    santa_vt_block<MODE, SV>(a, blockIdx.x);
   }
 }
 
@@ -2714,32 +2719,6 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
   if (tid == 0) *status = 0;
 }
 
-// santa_sp2_kernel's scaled units (see its solve loop): shift, key tie-break
-// field (class 1 | position key 8 | row-or-column 8 bits, n <= 256), bias
-// (keeps sb > 0: spc >= -n_wish * 2^32 units > -2^39), magnitude bound.
-constexpr int SP2_SH = 17;
-constexpr uint32_t SP2_TIE_MASK = (1u << SP2_SH) - 1u;
-constexpr uint64_t SP2_BIAS = 1ull << (39 + SP2_SH);
-constexpr int64_t SP2_LIM = 1ll << (42 + SP2_SH);
-
-struct Sp2Lds {
-  size_t ctype, own, ovfr, ovf, u, rem, rowc, total;
-};
-
-__host__ __device__ __forceinline__ Sp2Lds sp2_lds_layout() {
-  Sp2Lds L;
-  size_t o = 0;
-  L.ctype = o;  o += 256 * 2;                  // column gift types (old)
-  L.own = o;    o += 256;                      // code(i, i): row i's own (old) gift
-  L.ovfr = o;   o += 256 * 4;                  // overflow range per row
-  L.ovf = o;    o += (size_t)SP2_OVF_CAP * 2;  // overflow entries
-  L.u = o;      o += (256 + 64) * 8;           // row duals (+ a dump slot per lane)
-  L.rem = o;    o += 256;                      // scipy's `remaining`: column at position p
-  L.rowc = o;   o += (256 + 32) * 8;           // current row: C[i][j] per column + dump slots
-  L.total = o;
-  return L;
-}
-
 // T[q] for a wave-uniform q (one indexed VGPR move)
 // (both halves read with the same index and selected: no branch in the step)
 __device__ __forceinline__ uint32_t tile2_get(const u32x32 &T0, const u32x32 &T1, int q) {
@@ -2747,348 +2726,12 @@ __device__ __forceinline__ uint32_t tile2_get(const u32x32 &T0, const u32x32 &T1
   return (q & 32) ? b : a;
 }
 
-template <bool EXACT>
-__global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const unsigned char *rec_all) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int b = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int n = a.n;
-  const unsigned char *rec = rec_all + (size_t)b * SP2_REC;
-  if (*(const volatile int32_t *)(rec + SP2_REC_STATUS)) return;  // skipped / left to the fallback
-  const Sp2Lds L = sp2_lds_layout();
-  int16_t *ctype = (int16_t *)(smem + L.ctype);
-  uint8_t *own = smem + L.own;
-  uint32_t *ovfr = (uint32_t *)(smem + L.ovfr);
-  uint16_t *ovf = (uint16_t *)(smem + L.ovf);
-  int64_t *u_l = (int64_t *)(smem + L.u);
-  uint8_t *rem = smem + L.rem;
-  uint64_t *rowc = (uint64_t *)(smem + L.rowc);
-  const int x31 = lane & 31;
-
-  // -- the tile into VGPRs (16 coalesced 16-byte loads per lane), the rest to LDS
-  u32x32 T0, T1;
-  uint32_t ovb = 0;  // bit k: row 4 * lane + k has more than 32 hits (overflow list)
-  {
-    const uint4 *src = (const uint4 *)(rec + SP2_REC_TILE);
-    const int nq4 = (n + 15) >> 4;  // 16-byte words holding the block's rows
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      const uint4 v0 = (w < nq4) ? src[w * 64 + lane] : make_uint4(0, 0, 0, 0);
-      const uint4 v1 = (w + 8 < nq4) ? src[(w + 8) * 64 + lane] : make_uint4(0, 0, 0, 0);
-      T0[4 * w + 0] = v0.x; T0[4 * w + 1] = v0.y; T0[4 * w + 2] = v0.z; T0[4 * w + 3] = v0.w;
-      T1[4 * w + 0] = v1.x; T1[4 * w + 1] = v1.y; T1[4 * w + 2] = v1.z; T1[4 * w + 3] = v1.w;
-    }
-    const uint32_t *ro = (const uint32_t *)(rec + SP2_REC_OVF);
-    for (int x = lane; x < SP2_OVF_CAP / 2; x += WAVE) ((uint32_t *)ovf)[x] = ro[x];
-    const uint32_t *rr = (const uint32_t *)(rec + SP2_REC_OVFR);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t g = rr[4 * lane + k];
-      ovfr[4 * lane + k] = g;
-      ovb |= (4 * lane + k < n && (g >> 16) != 0u) ? 1u << k : 0u;
-    }
-    ((uint32_t *)own)[lane] = ((const uint32_t *)(rec + SP2_REC_OWN))[lane];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int r = 4 * lane + k;
-      if (r < n) ctype[r] = a.types[a.rows[(size_t)b * n + r]];
-    }
-  }
-  for (int r = lane; r < n; r += WAVE) u_l[r] = 0;
-  const int nw1 = a.n_wish + 1;
-  const int64_t E = a.E;
-  {
-    const u64x2 E2 = {(uint64_t)E << SP2_SH, (uint64_t)E << SP2_SH};
-    *(u64x2 *)(rowc + 4 * lane) = E2;
-    *(u64x2 *)(rowc + 4 * lane + 2) = E2;
-  }
-  __syncthreads();
-  __builtin_amdgcn_s_setprio(3);  // (lowered over the last Dijkstras, below)
-  const uint64_t m1 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
-
-  // -- solve (santa_sp_kernel's step; the row's hits come from the tile) -----------
-  // Scaled units: every cost, dual and path length is held times 2^SP2_SH, so
-  // the low SP2_SH bits of sb = spc + BIAS are zero and the argmin key is
-  // sb | tie-break bits -- exact, one OR per column (no clamp, no saturated
-  // band, no fallback argmin).  Exact while |values| < 2^(63 - SP2_SH - 2)
-  // units: Santa duals stay within 200 happiness units (2^38.7 units,
-  // measured), the row duals only grow and the column duals only fall, so
-  // the final duals and every Dijkstra's minVal bound all intermediate values;
-  // a block outside the range (or every block under SH_FLAG_TEST_RANGE) is
-  // left untouched and re-solved by the fallback launch.
-  constexpr bool exact = EXACT;  // (the two-pass argmin of the tests: its own instantiation)
-  const uint64_t BIAS = SP2_BIAS;
-  int64_t sb[4], W[4];  // spc + BIAS; -v   (columns 4*lane + k), scaled
-  i32x4 path, r4c;
-  uint32_t c4r = ~0u;   // column of row 4*lane + k in byte k (0xFF: none yet)
-  uint32_t lo[4];
-  uint64_t LM[4];       // live (remaining) columns, wave masks
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    W[k] = 0;
-    path[k] = -1;
-    r4c[k] = -1;
-  }
-  uint64_t LM0[4];     // the columns < n (every Dijkstra starts with them live)
-#pragma unroll
-  for (int k = 0; k < 4; ++k) LM0[k] = __builtin_amdgcn_ballot_w64(4 * lane + k < n);
-  uint32_t rem0 = 0;  // rem[p] = n - 1 - p for this lane's 4 positions
-#pragma unroll
-  for (int k = 0; k < 4; ++k) rem0 |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
-  int steps = 0;
-  int fallbacks = 0;
-  bool mvbig = (a.flags & SH_FLAG_TEST_RANGE) != 0;  // a Dijkstra's minVal out of range
-  if (a.flags & SH_FLAG_BUILD_ONLY) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) r4c[k] = 4 * lane + k;
-    c4r = (uint32_t)(4 * lane) * 0x01010101u + 0x03020100u;
-  } else {
-    for (int cur = 0; cur < n; ++cur) {
-      // Issue priority falls over the block's last Dijkstras (n-32, n-8, n-2):
-      // the four blocks sharing a SIMD share its VALU issue, and a block near
-      // its end has the least work left, so the blocks that lag behind (the
-      // long ones, which set the round's time) take the issue slots first.
-      // An approximation of longest-remaining-first: -14 % (round 0) / -12 %
-      // (round 10) per full round, profiles/r02g_setprio_ab.jsonl.
-      if (cur == n - 32) __builtin_amdgcn_s_setprio(2);
-      if (cur == n - 8) __builtin_amdgcn_s_setprio(1);
-      if (cur == n - 2) __builtin_amdgcn_s_setprio(0);
-      // Dijkstra set-up: remaining = [n-1 .. 0], all columns live.  (The lane
-      // id goes through an empty asm so that the per-column constants below
-      // are recomputed here rather than kept live, or spilled, across the loop.)
-      int ln = lane;
-      int64_t smax = INT64_MAX;  // (from SGPRs: no VGPR pair kept for the constant)
-      asm volatile("" : "+v"(ln), "+s"(smax));
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int j = 4 * ln + k;
-        const int pos = n - 1 - j;
-        sb[k] = smax;
-        // tie bits: unassigned (r4c < 0) 255 - pos | column, assigned 1 | pos | row
-        // (a bitfield select on the sign mask: no divergent branch)
-        const uint32_t um = (uint32_t)(r4c[k] >> 31);
-        const uint32_t la = ((uint32_t)(255 - pos) << 8) | (uint32_t)j;
-        const uint32_t lb = (1u << 16) | ((uint32_t)pos << 8) | (uint32_t)r4c[k];
-        lo[k] = (um & la) | (~um & lb);
-        LM[k] = LM0[k];
-      }
-      ((uint32_t *)rem)[lane] = rem0;
-      int nrem = n;
-      int64_t minVal = 0;
-      int i = cur;
-      int sink;
-      uint32_t kglo = ~0u;        // deferred: key bits of the previous winner
-      uint32_t kX = 0;            // deferred: position-key flip of the moved column
-      int kmover = -1;            //           ... and that column (a VGPR: the loaded byte as is)
-      for (;;) {
-        ++steps;
-        // row i: its tile entry (one indexed VGPR move), dual u[i] (LDS broadcast;
-        // u stays unchanged during a Dijkstra: the rows' updates are applied at
-        // its end from the removed columns)
-        const uint32_t tw = tile2_get(T0, T1, i >> 2);
-        const uint64_t uraw = (uint64_t)u_l[i];
-        const int mover_v = rem[nrem - 1];  // the column at the last position
-        const uint32_t e = (tw >> ((i & 1) << 4)) & 0xFFFFu;
-        // the row's half of the wave (lanes 32L.., L = (i >> 1) & 1) as an SGPR mask
-        const uint64_t hmask = ((i >> 1) & 1) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
-        const bool mine = __builtin_amdgcn_inverse_ballot_w64(hmask);
-        const uint32_t ea = e >> 9;
-        // previous step's book-keeping (no LDS dependence): the mover's position
-        // key first, in place, then the winner leaves the live masks (the moved
-        // column's new bits never equal the winner's: they differ in the row or
-        // column field, or the mover is the winner and its bits are unchanged)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) lo[k] ^= (4 * lane + k == kmover) ? kX : 0u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) LM[k] &= ~__builtin_amdgcn_ballot_w64(lo[k] == kglo);
-        // expand the row: hit columns get -a << 32, the rest hold E
-        const int sslot = mine ? (int)(e & 0x1FFu) : 256 + x31;
-        rowc[sslot] = (uint64_t)(uint32_t)(-(int)ea) << (32 + SP2_SH);
-        // (rows with more than 32 hits: a bit per row, read from the row's owner lane)
-        const bool ovr = (__builtin_amdgcn_readlane((int)ovb, i >> 2) >> (i & 3)) & 1;
-        if (__builtin_expect(ovr, 0)) {
-          const uint32_t rg = ovfr[i];  // more than 32 hits: the rest from the overflow area
-          const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
-          for (int x = lane; x < oc; x += WAVE) {
-            const uint32_t e2 = ovf[os + x];
-            rowc[e2 & 0x1FFu] = (uint64_t)(uint32_t)(-(int)(e2 >> 9)) << (32 + SP2_SH);
-          }
-        }
-        const u64x2 c01 = *(const u64x2 *)(rowc + 2 * lane);
-        const u64x2 c23 = *(const u64x2 *)(rowc + 128 + 2 * lane);
-        // un-scatter: the slots written above get E back (in-order LDS: after the reads)
-        rowc[sslot] = (uint64_t)E << SP2_SH;
-        if (__builtin_expect(ovr, 0)) {
-          const uint32_t rg = ovfr[i];
-          const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
-          for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = (uint64_t)E << SP2_SH;
-        }
-        const uint64_t cc[4] = {c01[0], c01[1], c23[0], c23[1]};
-        // u~[i] = u[i] - minVal (row i is reached at the current minimum)
-        const int64_t ui = (int64_t)rfl_u64(uraw) - minVal;
-        // r + BIAS = C[i][j] - u~[i] - v[j] + BIAS
-        uint64_t bse = BIAS - (uint64_t)ui;
-        asm volatile("" : "+s"(bse));  // keep (W + C) + bse one 64-bit add
-        uint64_t best = ~0ull;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint64_t r = ((uint64_t)W[k] + cc[k]) + bse;
-          const bool lv = __builtin_amdgcn_inverse_ballot_w64(LM[k]);
-          // (a removed column never improves: r >= minVal >= its spc by dual
-          // feasibility, so `upd` needs no live mask)
-          const bool upd = (int64_t)r < sb[k];
-          sb[k] = upd ? (int64_t)r : sb[k];
-          path[k] = upd ? i : path[k];
-          // (sb > 0: spc >= min C - v >= -n_wish * 2^32 units > -BIAS)
-          const uint64_t key = (uint64_t)sb[k] | lo[k];
-          best = (lv && key < best) ? key : best;
-        }
-        uint64_t g = rfl_u64(wave_min_u64_fast(best));
-        if (exact) {
-          // two-pass argmin (test path): min sb, then min tie-break bits
-          uint64_t m = ~0ull;
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (__builtin_amdgcn_inverse_ballot_w64(LM[k])) m = umin64(m, (uint64_t)sb[k] ^ SIGN64);
-          m = wave_min_u64_dpp(m);
-          const int64_t ms = (int64_t)(m ^ SIGN64);
-          uint64_t b2 = ~0ull;
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (__builtin_amdgcn_inverse_ballot_w64(LM[k]) && sb[k] == ms) b2 = umin64(b2, (uint64_t)lo[k]);
-          g = (uint64_t)ms | (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)wave_min_u64_dpp(b2));
-          ++fallbacks;
-        }
-        minVal = (int64_t)((g & ~(uint64_t)SP2_TIE_MASK) - BIAS);
-        const uint32_t glo = (uint32_t)g & SP2_TIE_MASK;
-        const bool assigned = (glo >> 16) & 1u;
-        const int pk = (int)((glo >> 8) & 255u);
-        const int aux = (int)(glo & 255u);
-        const int pstar = assigned ? pk : 255 - pk;
-        const int last = nrem - 1;
-        // the winner leaves `remaining`; the column at `last` moves to pstar
-        // (applied to the registers at the top of the next step)
-        kglo = glo;
-        kX = (uint32_t)(last ^ pstar) << 8;
-        kmover = mover_v;
-        rem[pstar] = (uint8_t)mover_v;  // (every lane, same byte; a no-op when pstar == last)
-        --nrem;
-        if (!assigned) {
-          sink = aux;
-          break;
-        }
-        i = aux;
-      }
-      // Dual update (scipy: u[cur] += minVal; u[i] += minVal - spc[col4row[i]]
-      // for the other visited rows; v[j] -= minVal - spc[j] for the removed
-      // columns).  The visited rows other than cur are the rows of the removed
-      // assigned columns, and a removed column's spc is frozen since its removal
-      // (it never improves again), so the column owners apply both updates;
-      // the matching makes the rows distinct.  Branch-free: every column adds
-      // its (masked) update with one LDS atomic add -- a visited column is
-      // assigned, the others add 0, unassigned ones to the lane's dump slot.
-      // (The pending removal of the sink needs no update: spc = minVal.)
-      const uint64_t mvb = (uint64_t)minVal + BIAS;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool vk = __builtin_amdgcn_inverse_ballot_w64(~LM[k] & LM0[k]);
-        const int64_t dd = vk ? (int64_t)(mvb - (uint64_t)sb[k]) : 0;
-        W[k] += dd;
-        const int ua = r4c[k] >= 0 ? r4c[k] : 256 + lane;
-        __hip_atomic_fetch_add((unsigned long long *)(u_l + ua), (unsigned long long)dd, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      if (lane == 0) u_l[cur] += minVal;
-      mvbig |= (uint64_t)(minVal + SP2_LIM) >= 2 * (uint64_t)SP2_LIM;
-      // augment along path[] from the sink back to cur (registers only)
-      int j = sink;
-      for (;;) {
-        const int jl = j >> 2;
-        const int p0 = __builtin_amdgcn_readlane(path[0], jl), p1 = __builtin_amdgcn_readlane(path[1], jl);
-        const int p2 = __builtin_amdgcn_readlane(path[2], jl), p3 = __builtin_amdgcn_readlane(path[3], jl);
-        const int pi = (j & 2) ? ((j & 1) ? p3 : p2) : ((j & 1) ? p1 : p0);
-        // row pi: its previous column t leaves, j becomes its column (scalar
-        // read-modify-write of the packed byte, one writelane)
-        const int pl = pi >> 2, ps = 8 * (pi & 3);
-        const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)c4r, pl);
-        const int t = (int)((cw >> ps) & 0xFFu);
-        const uint32_t nw4 = (cw & ~(0xFFu << ps)) | ((uint32_t)j << ps);
-        // (v_writelane with the lane select in M0: one SGPR operand per VOP3 on
-        // gfx950; the "{m0}" constraint makes the compiler load M0 itself)
-        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(c4r) : "s"(nw4), "{m0}"(pl));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) r4c[k] = (4 * lane + k == j) ? pi : r4c[k];
-        j = t;
-        if (pi == cur) break;
-      }
-    }
-  }
-  __syncthreads();
-
-  {  // the scaled-unit range (see the solve loop): leave the block to the fallback
-    bool big = mvbig;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      big |= (uint64_t)(W[k] + SP2_LIM) >= 2 * (uint64_t)SP2_LIM;
-      if (4 * lane + k < n) big |= (uint64_t)(u_l[4 * lane + k] + SP2_LIM) >= 2 * (uint64_t)SP2_LIM;
-    }
-    if (__builtin_expect(__any(big), 0)) {
-      if (lane == 0) {
-        const int p = atomicAdd(a.ovf_cnt, 1);
-        a.ovf_list[p] = b;
-      }
-      return;
-    }
-  }
-  const uint64_t m2 = (a.flags & SH_FLAG_TIMING) ? __builtin_amdgcn_s_memtime() : 0;
-  // -- outputs: lane handles rows i = 4*lane + k ------------------------------------
-  int64_t cost = 0, dch = 0, dgh = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int i = 4 * lane + k;
-    const int col = (int)((c4r >> (8 * k)) & 0xFFu);
-    int64_t vq[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) vq[q] = __shfl(-W[q], col >> 2, WAVE);
-    const int cs = col & 3;
-    const int64_t vcol = (cs == 0) ? vq[0] : (cs == 1) ? vq[1] : (cs == 2) ? vq[2] : vq[3];
-    if (i < n) {
-      const uint32_t co = own[i];
-      const int chd = a.rows[(size_t)b * n + i];
-      const int told = ctype[i], tnew = ctype[col];
-      if (a.flags & SH_FLAG_BUILD_ONLY) {
-        cost += single_cost(co, nw1, E);
-      } else {
-        const int64_t cij = (u_l[i] + vcol) >> SP2_SH;  // = C[i][col] (tight matched edge)
-        const uint32_t cn = (cij == E) ? 0u : (uint32_t)((cij >> 32) + nw1);
-        cost += cij;
-        dch += child_happy(cn, nw1) - child_happy(co, nw1);
-        if (a.delta) dgh += gift_happy(a, chd, tnew) - gift_happy(a, chd, told);
-      }
-      if (a.col) a.col[(size_t)b * n + i] = col;
-      if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[chd] = (int16_t)tnew;  // this block owns chd; ctype holds old types
-    }
-  }
-  cost = wave_sum_i64(cost);
-  dch = wave_sum_i64(dch);
-  dgh = wave_sum_i64(dgh);
-  if (lane == 0) {
-    if (a.cost) a.cost[b] = cost;
-    if (a.steps) a.steps[b] = steps;
-    if ((a.flags & SH_FLAG_TIMING) && a.col && n > 1)  // solve, shader cycles
-      a.col[(size_t)b * n + 1] = (int32_t)min(m2 - m1, (uint64_t)INT32_MAX);
-    if (a.delta) {
-      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
-      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
-    }
-    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
-  }
-}
-
 // ---------------------------------------------------------------------------
-// santa_sp3_kernel: santa_sp2_kernel's design (one wave per block, the hit
-// tile in 64 VGPRs, scipy's SAP decision for decision) with 32-bit values
-// and a 32-bit argmin key.
+// santa_sp3_kernel: one wave per block, the block's hit tile in 64 VGPRs
+// (santa_tile_kernel's record), scipy's SAP decision for decision with
+// 32-bit values and a 32-bit argmin key.  (Round 2's santa_sp2_kernel, the
+// same design in 64-bit scaled units, left the library in round 4: git
+// history, profiles/r03_sp3v5_ab.jsonl.)
 //
 // Lattice units.  Every value the solve forms is an integer combination of
 // the two Santa costs: a wish -a * 2^32 and a miss E (units of 2^-31), i.e.
@@ -3109,20 +2752,21 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp2_kernel(SantaArgs a, const u
 // leaves the range is left untouched for the fallback launch (never on the
 // synthetic Kaggle-shaped rounds, where m stays 0 on every dual:
 // tools/analysis/mrange.py; forced in the tests by SH_FLAG_TEST_RANGE).
-// Per step: ~50 VALU (santa_sp2_kernel: 108), no 64-bit LDS traffic.
+// Per step: ~70 VALU (round 2's 64-bit santa_sp2_kernel: 108), no 64-bit LDS traffic.
 // ---------------------------------------------------------------------------
 // TIMED (SH_FLAG_TIMING, dev): shader-clock cycles per segment of the solve,
 // summed over the block, in col[b * n + 0..3]: A = a step's row fetch, scatter
 // and LDS reads up to the relaxation's inputs; B = relaxation, key and argmin;
 // C = winner decode and book-keeping; D = per-Dijkstra set-up, dual update and
 // augmentation.  (s_memtime stamps cost cycles themselves: relative view.)
-// issue-priority steps of santa_sp3_kernel (Dijkstras before the last; see
-// santa_sp2_kernel; -D overrides are for A/B builds only)
-#ifndef SP3_PRIO_A
-#define SP3_PRIO_A 32
-#define SP3_PRIO_B 8
-#define SP3_PRIO_C 2
-#endif
+// Issue priority falls over the block's last Dijkstras (n-32, n-8, n-2): the
+// four blocks sharing a SIMD share its VALU issue, and a block near its end
+// has the least work left, so the blocks that lag behind (the long ones,
+// which set the round's time) take the issue slots first -- an approximation
+// of longest-remaining-first: -14 % (round 0) / -12 % (round 10) per full
+// round (profiles/r02g_setprio_ab.jsonl), re-checked on this kernel against
+// (64, 16, 4), (16, 4, 1) and none (profiles/r03_sp3_prio_ab.jsonl).
+constexpr int SP3_PRIO_A = 32, SP3_PRIO_B = 8, SP3_PRIO_C = 2;
 template <bool TIMED>
 __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const unsigned char *rec_all) {
   // (static LDS: every address below is a constant offset, no base register)
@@ -3140,7 +2784,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   if (*(const volatile int32_t *)(rec + SP2_REC_STATUS)) return;  // skipped / left to the fallback
   const int x31 = lane & 31;
 
-  // -- the tile into VGPRs (santa_sp2_kernel's record), the rest to LDS -------------
+  // -- the tile into VGPRs (santa_tile_kernel's record), the rest to LDS ------------
   u32x32 T0, T1;
   {
     const uint4 *src = (const uint4 *)(rec + SP2_REC_TILE);
@@ -3200,7 +2844,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
 #pragma unroll
   for (int k = 0; k < 4; ++k) rem0 |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
   int steps = 0;
-  bool bad = (a.flags & SH_FLAG_TEST_RANGE) != 0;  // the lattice range left (per-lane flag)
+  // the lattice range left (per-lane flag); SH_FLAG_TEST_RANGE and
+  // SH_FLAG_EXACT_ARGMIN send every block to the fallback launch (the
+  // windowed-key solver, whose two-pass argmin the latter selects)
+  bool bad = (a.flags & (SH_FLAG_TEST_RANGE | SH_FLAG_EXACT_ARGMIN)) != 0;
   uint32_t accm = 0, acca = 0;                     // range of every u~ a step read (see below)
   const int l4 = 4 * lane;
   int colk[4];  // this lane's columns (VGPR constants for the book-keeping compares)
@@ -3219,7 +2866,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
     c4r = (uint32_t)(4 * lane) * 0x01010101u + 0x03020100u;
   } else {
     for (int cur = 0; cur < n; ++cur) {
-      if (cur == n - SP3_PRIO_A) __builtin_amdgcn_s_setprio(2);  // (santa_sp2_kernel's issue priority)
+      if (cur == n - SP3_PRIO_A) __builtin_amdgcn_s_setprio(2);  // (issue priority, above)
       if (cur == n - SP3_PRIO_B) __builtin_amdgcn_s_setprio(1);
       if (cur == n - SP3_PRIO_C) __builtin_amdgcn_s_setprio(0);
       // Dijkstra set-up: remaining = [n-1 .. 0], every column < n live, spc = inf
@@ -3387,7 +3034,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         i = __builtin_amdgcn_readlane((int)rsel, lw);
         if (!assigned) break;
       }
-      // Dual update (santa_sp2_kernel's, in V units): the columns that left
+      // Dual update (scipy's, in V units, deferred to the Dijkstra's end): the columns that left
       // `remaining` (lo = ~0; not the sink, whose update is 0) add
       // minVal - spc to -v and to the dual of their row.
       const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
@@ -4256,7 +3903,11 @@ template <int MODE, int SV = 0>
 int launch_santa_vt(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
   const VtLds L = vt_lds_layout(ctx->ng);
   if (L.total > 64 * 1024) return fail(SH_ERR_ARGS, "too many gift types for the LDS chain heads");
-  hipLaunchKernelGGL((santa_vt_kernel<MODE, SV>), dim3(B), dim3(VT_WG), L.total, s, a);
+  // the fallback launch (SV = 0, a block list) loops over its list: one
+  // workgroup per CU
+  if ((SV == 0) != (a.blist != nullptr)) return fail(SH_ERR_ARGS, "santa_vt_kernel<0, 0> is the fallback launch only");
+  const int grid = a.blist ? std::max(1, std::min(B, ctx->n_cu)) : B;
+  hipLaunchKernelGGL((santa_vt_kernel<MODE, SV>), dim3(grid), dim3(VT_WG), L.total, s, a);
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
@@ -4343,7 +3994,7 @@ int launch_santa_vt_sc(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   a.ovf_cnt = ctx->d_ovf + p;
   a.ovf_list = ctx->d_ovf + 2 + (size_t)p * ctx->ovf_cap;
   a.blist = nullptr;
-  int rc = (a.flags & SH_FLAG_SP2) ? launch_santa_vt<0, 2>(ctx, a, B, s) : launch_santa_vt<0, 1>(ctx, a, B, s);
+  int rc = launch_santa_vt<0, 1>(ctx, a, B, s);
   if (rc == SH_OK) {
     SantaArgs f = a;
     f.blist = a.ovf_list;
@@ -4392,14 +4043,7 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
     else
       hipLaunchKernelGGL(santa_tile_kernel<0>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
     HIP_TRY(hipGetLastError());
-    if (a.flags & SH_FLAG_EXACT_ARGMIN)
-      hipLaunchKernelGGL(santa_sp2_kernel<true>, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
-                         (const unsigned char *)ctx->d_rec);
-    else if (a.flags & SH_FLAG_SP2)
-      hipLaunchKernelGGL(santa_sp2_kernel<false>, dim3(B), dim3(WAVE), sp2_lds_layout().total, s, a,
-                         (const unsigned char *)ctx->d_rec);
-    else
-      if (a.flags & SH_FLAG_TIMING)
+    if (a.flags & SH_FLAG_TIMING)
         hipLaunchKernelGGL(santa_sp3_kernel<true>, dim3(B), dim3(WAVE), 0, s, a, (const unsigned char *)ctx->d_rec);
       else
         hipLaunchKernelGGL(santa_sp3_kernel<false>, dim3(B), dim3(WAVE), 0, s, a, (const unsigned char *)ctx->d_rec);
@@ -4425,6 +4069,17 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
 }  // namespace
 
 namespace {
+// Flags of designs that left the library: SH_FLAG_SW_TILE (the one-wave
+// register-tile kernel, round 3), SH_FLAG_SP2 (santa_sp2_kernel, round 2's
+// 64-bit-key one-wave kernel, round 4).
+int refuse_retired(unsigned flags) {
+  if (flags & SH_FLAG_SW_TILE)
+    return fail(SH_ERR_ARGS, "SH_FLAG_SW_TILE: the one-wave register-tile design is retired");
+  if (flags & SH_FLAG_SP2)
+    return fail(SH_ERR_ARGS, "SH_FLAG_SP2: the 64-bit-key one-wave design (santa_sp2_kernel) is retired");
+  return SH_OK;
+}
+
 // LDS-tile blocks (singles, 4 waves) the device holds at once for this n.
 int lds_tile_slots(sh_ctx *ctx, int n) {
   if (ctx->lds_slots_n == n) return ctx->lds_slots;
@@ -4468,8 +4123,7 @@ int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   if ((flags & SH_FLAG_VT_TILE) || ctx->nc > (1 << 20) || ctx->ng > 1022) return SH_DESIGN_VT_TILE;
   // the register-tile sparse kernel keeps the wish value in 7 bits with one
   // code reserved (n_wish <= 126); the LDS-list kernel takes the rest
-  const int sparse = (ctx->n_wish > 126 || (flags & SH_FLAG_SP1)) ? SH_DESIGN_SPARSE
-                     : (flags & (SH_FLAG_SP2 | SH_FLAG_EXACT_ARGMIN)) ? SH_DESIGN_SPARSE2 : SH_DESIGN_SPARSE3;
+  const int sparse = (ctx->n_wish > 126 || (flags & SH_FLAG_SP1)) ? SH_DESIGN_SPARSE : SH_DESIGN_SPARSE3;
   if (flags & (SH_FLAG_SP_TILE | SH_FLAG_SP1)) return sparse;
   // few blocks (at most one resident wave of LDS-tile blocks): every block
   // starts at once and the launch takes one block's latency, which the
@@ -4513,7 +4167,6 @@ int resident_blocks(sh_ctx *ctx, int design, int mode, int n, int B) {
       return occ_blocks(ctx, santa_block_kernel<1, 1>, SANTA_WG, santa_lds_layout(n, 1, ctx->ng).total);
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
     case SH_DESIGN_VT_TILE: return vt_tile_slots(ctx);
-    case SH_DESIGN_SPARSE2: return occ_blocks(ctx, santa_sp2_kernel<false>, WAVE, sp2_lds_layout().total);
     case SH_DESIGN_SPARSE3: return occ_blocks(ctx, santa_sp3_kernel<false>, WAVE, 0);
     default:
       return occ_blocks(ctx, santa_sp_kernel<true>, WAVE, sp_lds_layout(ctx->ng, sp_capacity(ctx)).total);
@@ -4532,7 +4185,7 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   if (n <= 0 || n > SH_MAX_N_SANTA) return fail(SH_ERR_ARGS, "n must be in [1, 4096]");
   if ((int64_t)n * (mode + 1) > ctx->nc) return fail(SH_ERR_ARGS, "block larger than the instance");
   if (B < 0) return fail(SH_ERR_ARGS, "B < 0");
-  if (flags & SH_FLAG_SW_TILE) return fail(SH_ERR_ARGS, "SH_FLAG_SW_TILE: the one-wave register-tile design is retired");
+  HIP_TRY_RC(refuse_retired(flags));
   if (B == 0) return SH_OK;
   DeviceGuard dg(ctx->device);
   SantaArgs a;
@@ -4552,7 +4205,6 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
     case SH_DESIGN_LDS_TILE:
       return (flags & SH_FLAG_TIMING) ? launch_santa<1, 0, true>(ctx, a, B, s) : launch_santa<1, 0>(ctx, a, B, s);
     case SH_DESIGN_VT_TILE: return launch_santa_vt_sc(ctx, a, B, s);
-    case SH_DESIGN_SPARSE2:
     case SH_DESIGN_SPARSE3: return launch_santa_sp(ctx, a, B, s, true);
     default: return launch_santa_sp(ctx, a, B, s, false);
   }
@@ -4563,7 +4215,7 @@ int sh_solve_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS && mode != SH_MODE_TRIPLETS)
     return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA || B < 0) return fail(SH_ERR_ARGS, "bad n or B");
-  if (flags & SH_FLAG_SW_TILE) return fail(SH_ERR_ARGS, "SH_FLAG_SW_TILE: the one-wave register-tile design is retired");
+  HIP_TRY_RC(refuse_retired(flags));
   DeviceGuard dg(ctx->device);
   return pick_design(ctx, mode, n, B, flags);
 }
@@ -4574,7 +4226,7 @@ int sh_resident_blocks(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
     return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA || B < 0) return fail(SH_ERR_ARGS, "bad n or B");
   DeviceGuard dg(ctx->device);
-  if (flags & SH_FLAG_SW_TILE) return fail(SH_ERR_ARGS, "SH_FLAG_SW_TILE: the one-wave register-tile design is retired");
+  HIP_TRY_RC(refuse_retired(flags));
   return resident_blocks(ctx, pick_design(ctx, mode, n, B, flags), mode, n, B);
 }
 

@@ -30,7 +30,7 @@ SH_FLAG_SP_TILE = 128
 SH_FLAG_SP1 = 256
 SH_FLAG_TEST_RANGE = 512  # test hook: every register-tile block goes to the fallback launch
 SH_FLAG_NO_APPLY = 1024  # solve without writing the gift types (overlapping blocks allowed)
-SH_FLAG_SP2 = 2048  # A/B: the 64-bit-key register-tile solver (round 2 default)
+SH_FLAG_SP2 = 2048  # retired (round 4): the C-ABI refuses it (SH_ERR_ARGS)
 SH_ERRF_ROWS = 1
 SH_ERRF_INFEASIBLE = 2
 SH_ERRF_TYPE = 4
@@ -46,7 +46,7 @@ SH_DESIGN_NAMES = {0: "santa_sp_kernel (1-wave sparse LDS tile)", 1: "santa_bloc
                    2: "(retired: santa_sw_kernel)", 3: "santa_vt_kernel (4-wave register tile)",
                    4: "santa_block_kernel (twins, 4-wave code-pair tile)",
                    5: "santa_big_kernel (row rebuilt from the wishlist)",
-                   6: "santa_sp2_kernel (1-wave sparse register tile, 64-bit keys)",
+                   6: "(retired: santa_sp2_kernel)",
                    7: "santa_sp3_kernel (1-wave sparse register tile, 32-bit lattice keys)"}
 SH_MAX_N = 1024
 SH_MAX_N_SANTA = 4096

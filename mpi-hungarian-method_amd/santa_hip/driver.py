@@ -94,6 +94,7 @@ class LoopResult:
     best_score: float = float("-inf")
     rounds: int = 0
     blocks_solved: int = 0
+    sums: tuple | None = None  # exact (S_child, S_gift) of the final state
 
 
 def exchange(engine, world: World, mode: int, rows: torch.Tensor, n: int, B: int,
@@ -121,13 +122,28 @@ def exchange(engine, world: World, mode: int, rows: torch.Tensor, n: int, B: int
     engine.unpack_types(types, rows[:B * n], recv[:B * n], mode)
 
 
-def check_engine_errors(engine) -> None:
+ERROR_FLAG_BITS = 8  # SH_ERRF_* bits agreed across ranks (include/santa_hip.h)
+
+
+def check_engine_errors(engine, world: World | None = None, device=None) -> None:
     """Raise if the device flagged a skipped block since the last check (an
     out-of-range child id or gift type, an infeasible solve: the kernels
     leave such a block's types unchanged, which would otherwise be scored
-    and accepted silently).  Synchronises the engine's stream."""
+    and accepted silently).  Synchronises the engine's stream.
+
+    With several ranks every rank must call this at the same point: the
+    flags are agreed first (one all-reduce(MAX) of one int per flag bit:
+    NCCL/RCCL has no bitwise-or reduction), so either every rank raises or
+    none does -- a rank raising alone would leave the others waiting in the
+    next collective."""
     read = getattr(engine, "error_flags", None)
     flags = read() if read is not None else 0
+    if world is not None and world.distributed:
+        import torch.distributed as dist
+        bits = torch.tensor([(flags >> i) & 1 for i in range(ERROR_FLAG_BITS)], dtype=torch.int64,
+                            device=device)
+        dist.all_reduce(bits, op=dist.ReduceOp.MAX, group=world.group)
+        flags = sum(int(b) << i for i, b in enumerate(bits.tolist()))
     if flags:
         raise RuntimeError(f"sh_solve_blocks skipped blocks (device error flags {flags:#x}: "
                            "1 = child id out of range, 2 = infeasible, 4 = gift type out of range)")
@@ -184,6 +200,23 @@ class _Sums:
             raise RuntimeError(f"round {rnd}: delta sums ({sc}, {sg}) != full rescore ({full[0]}, {full[1]})")
         return full
 
+    def final_check(self, types, cur, history) -> None:
+        """The loop ended (round budget or patience stop): unless the last
+        round was a kept check round, its full rescore having confirmed `cur`,
+        rescore the final state once; it must equal `cur`, and the family
+        checks (mpi_single.py:32-44), which delta rounds skip, must pass."""
+        if not self.delta or not history:
+            return
+        last = history[-1]
+        if last.accepted and self.check_round(last.round):
+            return
+        full = tuple(self.engine.score_sums(types))
+        if (full[0], full[1]) != tuple(cur):
+            raise RuntimeError(f"final state: delta sums ({cur[0]}, {cur[1]}) != full rescore "
+                               f"({full[0]}, {full[1]})")
+        if full[2] or full[3]:
+            raise AssertionError("triplets/twins must share a gift (mpi_single.py:32-44)")
+
 
 def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, n: int = 256,
                blocks_per_round: int | None = None, seed: int = 2017, max_rounds: int = 100,
@@ -222,6 +255,8 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
                          "raises IndexError at mpi_twins.py:132)")
     res = LoopResult()
     sums = _Sums(engine, world, score_check_every, max_rounds)
+    if getattr(engine, "error_flags", None) is not None:
+        engine.error_flags()  # the flags cover this run only: drop what earlier calls left
     if sums0 is None and (score0 is None or sums.delta):
         sums0 = tuple(engine.score_sums(types)[:2])
     if score0 is None:
@@ -236,7 +271,8 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
     if pipeline and hasattr(engine, "score_begin"):
         res = _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
                              on_round, best, check_disjoint, res, accept, sums, cur)
-        check_engine_errors(engine)
+        check_engine_errors(engine, world, types.device)
+        sums.final_check(types, res.sums, res.history)
         return res
     for rnd in range(max_rounds):
         t0 = time.perf_counter()
@@ -251,7 +287,7 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
         if world.distributed:
             exchange(engine, world, mode, rows, n, B, types, buffers)
         if check_disjoint:
-            check_engine_errors(engine)
+            check_engine_errors(engine, world, types.device)
         if sums.delta:
             sums.reduce(d)
             sc, sg, bad_tri, bad_tw = sums.combine(
@@ -282,7 +318,9 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
         if count > patience:
             break
     res.best_score = best
-    check_engine_errors(engine)
+    res.sums = cur
+    check_engine_errors(engine, world, types.device)
+    sums.final_check(types, cur, res.history)
     return res
 
 
@@ -315,7 +353,7 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
         if world.distributed:
             exchange(engine, world, mode, rows, n, B, types, buffers)
         if check_disjoint:
-            check_engine_errors(engine)
+            check_engine_errors(engine, world, types.device)
         if sums.delta:
             sums.reduce(d)
             return engine.delta_begin(types, d, sums.check_round(r))
@@ -367,6 +405,7 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
         pending = (rnd, handle, t0, k) if handle is not None else None
         rnd += 1
     res.best_score = best
+    res.sums = cur
     return res
 
 

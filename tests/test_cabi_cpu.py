@@ -225,8 +225,8 @@ def test_bench_roofline_helpers():
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    assert bench.design_kernels("santa_sp2_kernel (1-wave sparse register tile)") == \
-        ["santa_tile_kernel", "santa_sp2_kernel"]
+    assert bench.design_kernels("santa_sp3_kernel (1-wave sparse register tile)") == \
+        ["santa_tile_kernel", "santa_sp3_kernel"]
     assert bench.design_kernels("santa_block_kernel (twins, 4-wave code-pair tile)") == ["santa_block_kernel"]
     for blocks in (78, 466, 467, 12345):
         t = bench.stored_traffic(["santa_block_kernel"], blocks)
@@ -238,7 +238,7 @@ def test_bench_roofline_helpers():
             s = json.load(open(os.path.join(root, "profiles", o["source"].split(" ")[0])))
             assert s["probe"]["blocks"] == blocks
     assert bench.stored_traffic(["santa_block_kernel"], 12345)["traffic"] is None
-    t = bench.stored_traffic(["santa_tile_kernel", "santa_sp2_kernel"], 3730)
+    t = bench.stored_traffic(["santa_tile_kernel", "santa_sp3_kernel"], 3730)
     if t["traffic"] is None:
         assert "kernel source" in t["traffic_note"]
     else:
@@ -247,4 +247,4 @@ def test_bench_roofline_helpers():
         hb = s["hbm_bytes_per_launch"]
         est = sum(hb[k]["FETCH_SIZE_bytes"] * f for k, f in zip(raw["kernels"], raw["fetch_correction"]))
         assert t["traffic"] == round(est + raw["WRITE_SIZE"])
-        assert raw["kernels"] == ["santa_tile_kernel", "santa_sp2_kernel"]
+        assert raw["kernels"] == ["santa_tile_kernel", "santa_sp3_kernel"]

@@ -277,3 +277,99 @@ def test_delta_mismatch_raises(pipeline):
         run_rounds(Off(sd.wish, sd.goodkids, sd.nq), torch.from_numpy(sd.types.copy()), mode=0, n=64,
                    seed=1, max_rounds=5, patience=100, world=World(), pipeline=pipeline,
                    score_check_every=2)
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_patience_stop_is_checked_against_a_full_rescore(pipeline):
+    """A run that stops on patience before its next check round still ends
+    with a full rescore of the final state: a wrong delta cannot reach the
+    final sums unverified (K larger than the rounds the run lasts)."""
+    from cpu_engine import CPUOracleEngine
+    sd = D.synthetic(**SMALL)
+
+    class Off(CPUOracleEngine):
+        def solve_blocks(self, mode, rows, n, types, delta=None):
+            super().solve_blocks(mode, rows, n, types, delta=delta)
+            if delta is not None:
+                delta[1] += 1
+
+    with pytest.raises(RuntimeError, match="final state"):
+        run_rounds(Off(sd.wish, sd.goodkids, sd.nq), torch.from_numpy(sd.types.copy()), mode=0, n=64,
+                   seed=1, max_rounds=50, patience=-1, world=World(), pipeline=pipeline,
+                   score_check_every=40)
+    # an honest engine passes the same final check and reports the final sums
+    eng = CPUOracleEngine(sd.wish, sd.goodkids, sd.nq)
+    t = torch.from_numpy(sd.types.copy())
+    res = run_rounds(eng, t, mode=1, n=16, seed=1, max_rounds=50, patience=-1, world=World(),
+                     pipeline=pipeline, score_check_every=40)
+    assert res.rounds == 1
+    assert res.sums == tuple(eng.score_sums(t)[:2])
+
+
+def test_stale_error_flags_do_not_fail_a_new_run():
+    """Flags left by an earlier, unrelated call on the same engine are read and
+    dropped when run_rounds starts; flags raised during the run still fail it."""
+    from cpu_engine import CPUOracleEngine
+    sd = D.synthetic(**SMALL)
+
+    class Stale(CPUOracleEngine):
+        pending = _lib.SH_ERRF_TYPE
+
+        def error_flags(self):
+            f, self.pending = self.pending, 0
+            return f
+
+    eng = Stale(sd.wish, sd.goodkids, sd.nq)
+    res = run_rounds(eng, torch.from_numpy(sd.types.copy()), mode=0, n=64, seed=1, max_rounds=2,
+                     patience=100, world=World())
+    assert res.rounds == 2
+
+
+def _flag_worker(rank, size, port, pipeline, check, out):
+    import datetime
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    for p in (os.path.join(root, "mpi-hungarian-method_amd"), os.path.join(root, "oracle"), here):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from cpu_engine import CPUOracleEngine
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=size, timeout=datetime.timedelta(seconds=60))
+    sd = D.synthetic(**SMALL)
+
+    class OneRankFlags(CPUOracleEngine):
+        solved = 0
+
+        def solve_blocks(self, *a, **kw):
+            self.solved += 1
+            return super().solve_blocks(*a, **kw)
+
+        def error_flags(self):  # only rank 1's device saw a bad block, from its first round on
+            return _lib.SH_ERRF_TYPE if rank == 1 and self.solved else 0
+
+    eng = OneRankFlags(sd.wish, sd.goodkids, sd.nq)
+    try:
+        run_rounds(eng, torch.from_numpy(sd.types.copy()), mode=0, n=64, seed=1, max_rounds=3,
+                   patience=100, world=World(rank, size, None), pipeline=pipeline, check_disjoint=check)
+        out[rank] = ("ok", eng.solved)
+    except RuntimeError as e:
+        out[rank] = (str(e), eng.solved)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pipeline,check", [(False, True), (True, True), (False, False), (True, False)])
+def test_error_flags_agreed_across_ranks(pipeline, check):
+    """Only one rank's device flags a skipped block: every rank raises at the
+    same point (the flags are all-reduced before anyone raises), so no rank is
+    left waiting in a collective (the 60 s gloo timeout would fail this)."""
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_flag_worker, args=(2, port, pipeline, check, out), nprocs=2, join=True)
+    for r in range(2):
+        msg, solved = out[r]
+        assert "error flags 0x4" in msg, (r, msg)
+        assert solved == (1 if check else 3), (r, solved)
