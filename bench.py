@@ -290,14 +290,18 @@ def design_kernels(kname: str):
     return ["santa_tile_kernel", k] if k == "santa_sp3_kernel" else [k]
 
 
-def _same_launch(s, blocks):
+def _same_launch(s, blocks, n=256, mode=0):
     """A summary describes this launch only if its probe ran the same number
-    of blocks per launch (one kernel name covers several workloads: the 4-wave
-    santa_block_kernel runs the twins round and the 8-GPU singles shard)."""
-    return s.get("probe", {}).get("blocks") == blocks
+    of blocks per launch of the same block size and mode (one kernel name
+    covers several workloads: the 4-wave santa_block_kernel runs the twins
+    round and the 8-GPU singles shard; santa_big_kernel every n > 256).
+    (Summaries from before round 4 recorded no n / mode: n = 256, and the
+    mode is implied by the block count.)"""
+    p = s.get("probe", {})
+    return p.get("blocks") == blocks and p.get("n", 256) == n and p.get("mode", mode) == mode
 
 
-def stored_occupancy(kname: str, blocks: int):
+def stored_occupancy(kname: str, blocks: int, n: int = 256, mode: int = 0):
     """Mean resident waves per SIMD and LDS-array activity of `kname` from
     the newest committed PMC summary of THIS kernel source and launch size
     (the "occ" pass of tools/profile_round.sh, round-0 launch), or None."""
@@ -307,14 +311,14 @@ def stored_occupancy(kname: str, blocks: int):
             s = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if s.get("source_sha16") == src and _same_launch(s, blocks) and kname in s.get("occupancy_lds", {}):
+        if s.get("source_sha16") == src and _same_launch(s, blocks, n, mode) and kname in s.get("occupancy_lds", {}):
             e = dict(s["occupancy_lds"][kname])
             e["source"] = f"{os.path.basename(path)} (round-0 launch, kernel source {src})"
             return e
     return None
 
 
-def stored_traffic(knames, blocks: int):
+def stored_traffic(knames, blocks: int, n: int = 256, mode: int = 0):
     """HBM bytes per launch of the kernels `knames` (summed) from the newest committed rocprofv3 PMC
     summary taken on THIS kernel source (tools/profile_round.sh ->
     profiles/<tag>_summary.json records the source hash).  Each kernel's
@@ -330,7 +334,7 @@ def stored_traffic(knames, blocks: int):
             s = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if s.get("source_sha16") != src or not _same_launch(s, blocks):
+        if s.get("source_sha16") != src or not _same_launch(s, blocks, n, mode):
             continue
         hb = s.get("hbm_bytes_per_launch", {})
         es = [hb.get(k, {}) for k in knames]
@@ -347,7 +351,7 @@ def stored_traffic(knames, blocks: int):
                     "traffic_source": f"{os.path.basename(path)} (kernel source {src})"}
     return {"traffic": None,
             "traffic_note": f"no committed PMC summary was taken on this kernel source ({src}) "
-                            f"at {blocks} blocks per launch"}
+                            f"at {blocks} blocks of n = {n} per launch"}
 
 
 # --------------------------------------------------------------------------- main
@@ -519,7 +523,7 @@ def main():
             lds = {"bound": "lds", "achieved": round(ach, 3), "peak": round(LDS_PEAK_TBS, 1), "unit": "TB/s",
                    "frac": round(ach / LDS_PEAK_TBS, 4), "bytes_per_step": per_step, "bytes_per_dijkstra": per_dij,
                    "note": "algorithmic LDS bytes of the solve (steps of the timed launches) / kernel time"}
-            occ = stored_occupancy(kshort, my_blocks)
+            occ = stored_occupancy(kshort, my_blocks, n, mode)
             if occ:
                 lds["pmc"] = occ
         latency = {"steps_per_launch": float(st.sum(axis=1).mean()),
@@ -577,7 +581,7 @@ def main():
     # PMC summaries of the same kernel source and launch size: the full one-GPU
     # round (tools/profile_round.sh) or rank 0's shard at N = 2, 4, 8
     # (tools/profile_shards.sh); else a traffic_note says none was taken
-    out["roofline"].update(stored_traffic(design_kernels(kname), my_blocks))
+    out["roofline"].update(stored_traffic(design_kernels(kname), my_blocks, n, mode))
     if cpu_line is not None:
         out["cpu_baseline"] = cpu_line
     if rank == 0:

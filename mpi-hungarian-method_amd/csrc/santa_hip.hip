@@ -388,7 +388,8 @@ struct SolveLds {
   int16_t *c4r;     // [n]   col4row (the result)
   int16_t *r4c;     // [n]   row4col
   int16_t *path;    // [n]   path dump of the visited columns
-  uint64_t *red;    // [4 * NW]  step argmin words (3, rotating) + fallback partials [2NW, 4NW)
+  uint64_t *red;    // [4 * NW]  step argmin words (3, rotating) + fallback partials [2NW, 4NW);
+                    // sap_solve_mw_sc: [SC_RING] words (a ring, re-armed in halves)
 };
 
 template <int NW>
@@ -600,6 +601,14 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
 // Returns true (block-wide) when a bound was crossed: the caller re-solves
 // with sap_solve_mw.  The loader returns costs scaled by 2^SC_SH.
 // ---------------------------------------------------------------------------
+// sap_solve_mw_sc's step words: a ring of SC_RING, step s folding into word
+// s % SC_RING; after the barrier of a step s with s % (SC_RING / 2) == 0 the
+// lanes of wave 0 re-arm the other half (its words were last read before
+// that barrier and are next folded SC_RING / 2 steps later).  Round 3 re-armed
+// the next of three rotating words every step (an exec-masked single-lane
+// store and its address: ~9 instructions per step on the twins chain).
+constexpr int SC_RING = 64;
+static_assert(SC_RING == 64, "sap_solve_mw_sc's re-arm asm tests st & 31");
 constexpr int SC_SH = 17;
 constexpr uint32_t SC_TIE_MASK = (1u << SC_SH) - 1u;
 constexpr uint64_t SC_BIAS = 1ull << (41 + SC_SH);
@@ -613,12 +622,12 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
   int64_t sb = INT64_MAX, W = 0;  // spc + SC_BIAS; -v (this thread's column)
   int path = -1, pos = -1, r4c = -1;
   uint32_t lo = 0;
-  int64_t steps = 0;
-  int par = 0;  // rotating step-argmin word (0..2), as sap_solve_mw
+  int steps = 0;  // (also the ring position of the step word)
   const uint32_t wbase = lds_addr(S.red);
+  uint32_t tid8 = 8u * (uint32_t)(tid & 31);  // (the re-arm's word offset)
   uint64_t ones = ~0ull;
-  asm volatile("" : "+v"(ones));
-  if (tid < 3) S.red[tid] = ~0ull;
+  asm volatile("" : "+v"(tid8), "+v"(ones));
+  if (tid < SC_RING) S.red[tid] = ~0ull;
   __syncthreads();
   for (int cur = 0; cur < n; ++cur) {
     sb = INT64_MAX;
@@ -636,25 +645,10 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
     int pstar = -2, last = -3;
     uint32_t kX = 0;
     for (;;) {
-      ++steps;
+      const int st = steps++;  // (this step's ring word: st % SC_RING)
       const uint64_t uraw = (uint64_t)S.u[i];
       int64_t c[1];
       ld.load(i, c, la...);
-      {
-        // re-arm the next step's word: lane 0 of every wave writes ~0 (the
-        // word was last read before barrier t - 1, is next folded after
-        // barrier t; the fold's wait below covers this write)
-        const uint32_t wn = wbase + 8u * (uint32_t)(par == 2 ? 0 : par + 1);
-        uint64_t sv;
-        asm volatile(
-            "s_mov_b64 %0, exec\n\t"
-            "s_mov_b64 exec, 1\n\t"
-            "ds_write_b64 %1, %2\n\t"
-            "s_mov_b64 exec, %0"
-            : "=&s"(sv)
-            : "v"(wn), "v"(ones)
-            : "memory");
-      }
       {
         const bool isW = pos == pstar, isM = pos == last;
         lo ^= isM ? kX : 0u;  // (kX = 0 when the mover is the winner)
@@ -678,8 +672,8 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
       // the atomic is in the asm: the compiler's waitcnt before the barrier
       // does not see LDS ops issued by inline asm)
       const uint32_t mh = row_min_u32_dpp(bh);
+      const uint32_t wa = wbase + 8u * (uint32_t)(st & (SC_RING - 1));
       {
-        const uint32_t wa = wbase + 8u * (uint32_t)par;
         uint64_t sv, m0, m1;
         asm volatile(
             "v_cmp_eq_u32_e64 %1, %3, %4\n\t"
@@ -694,8 +688,28 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
             : "memory");
       }
       __syncthreads();
-      const uint64_t g = S.red[par];
-      par = (par == 2) ? 0 : par + 1;
+      uint64_t g;
+      asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(g) : "v"(wa) : "memory");
+      {
+        // every SC_RING / 2 steps: re-arm the other half of the ring, words
+        // ((st + 32) % 64 + tid % 32) (every thread writes ~0; a scalar
+        // branch, not the exec-masked store on every step the compiler made
+        // of an if; the address is formed inside the branch)
+        uint32_t t, v;
+        asm volatile(
+            "s_and_b32 %0, %2, 31\n\t"  // (SC_RING / 2 - 1)
+            "s_cbranch_scc1 1f\n\t"
+            "s_lshl_b32 %0, %2, 3\n\t"
+            "s_xor_b32 %0, %0, 256\n\t"  // (8 * SC_RING / 2)
+            "s_and_b32 %0, %0, 504\n\t"  // (8 * (SC_RING - 1))
+            "s_add_u32 %0, %0, %3\n\t"
+            "v_add_u32 %1, %0, %4\n\t"
+            "ds_write_b64 %1, %5\n"
+            "1:"
+            : "=&s"(t), "=&v"(v)
+            : "s"(st), "s"(wbase), "v"(tid8), "v"(ones)
+            : "memory", "scc");
+      }
       const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32));
       uint32_t glo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
       asm volatile("" : "+s"(glo));
@@ -751,11 +765,31 @@ constexpr int SP3_SH = 11;                  // key tie-break field: class 1 | pk
 constexpr int32_t SP3_BIAS = 1 << 20;       // spc_V + BIAS in [0, 2^21) (key field)
 constexpr uint32_t SP3_INF = (1u << 21) - 1u;  // "infinite" spc (never a live winner)
 
-// V = A * 512 + m with |A| <= amax and |m| <= mmax (2 * mmax < 512)
-__device__ __forceinline__ bool sp3_in_range(int32_t V, int amax, int mmax) {
-  return (((uint32_t)(V + mmax) & 511u) <= (uint32_t)(2 * mmax)) &&
-         ((uint32_t)(V + amax * 512 + mmax) <= (uint32_t)(2 * (amax * 512 + mmax)));
-}
+// The lattice range as OR-accumulated bit tests (round 4): a value V passes
+// when t = V + C has no bit of MASK set, i.e. t < 2^H (|A| < 2^(H - 10)) and
+// (m + 2^b - 1) mod 512 < 2^(b + 1) (m in [1 - 2^b, 2^b]); OR-ing the t of
+// every value and testing once at the end checks them all -- two SALU per
+// step (add, or) instead of five (the max / abs / and of two running maxima).
+// Bounds: row duals as read by a step (u~ = u - minVal) |A| < 1024, |m| <= 2^bU;
+// column duals (W = -v, per Dijkstra) |A| < 512, |m| <= 2^cW; so every
+// relaxation value has |A| <= 512 + 100 + 1024 < 2048 (the key's 21-bit field
+// around BIAS = 2^20) and |m| <= 2^cW + 1 + 2^bU <= M (the lattice bound).
+// Santa rounds stay far inside: max |A| of u, v, minVal 100 / 46 / 100 and
+// m = 0 on every dual (tools/analysis/mrange.py, bench rounds 0..19).
+struct LatticeRange {
+  uint32_t CU, MU, CW, MW;
+  bool ok;  // M >= 3 (n_wish >= 2): else every block takes the fallback
+  __device__ __forceinline__ explicit LatticeRange(int M) {
+    const int m3 = max(1, (M - 1) / 3);
+    const int cw = 31 - __builtin_clz((uint32_t)m3);
+    const int bu = 31 - __builtin_clz((uint32_t)max(1, M - 1 - (1 << cw)));
+    ok = (1 << cw) + 1 + (1 << bu) <= M;
+    CU = (1u << 19) + (1u << bu) - 1u;
+    MU = 0xFFF00000u | (511u & ~((2u << bu) - 1u));
+    CW = (1u << 18) + (1u << cw) - 1u;
+    MW = 0xFFF80000u | (511u & ~((2u << cw) - 1u));
+  }
+};
 
 // ---------------------------------------------------------------------------
 // sap_solve_mw_l32: sap_solve_mw_sc's decisions in santa_sp3_kernel's 32-bit
@@ -780,13 +814,14 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
   const bool colv = j < n;
   int32_t *u32 = (int32_t *)S.u;
   const int Mm = (int)min((int64_t)199, (int64_t)(0xFFFFFFFFll / E) / 2);
-  const int mW = (Mm - 1) / 3, mU = Mm - 1 - mW;
+  const LatticeRange LR(Mm);
+  big |= !LR.ok;
   const uint32_t wa = lds_addr(S.red);  // the step word (LDS byte address)
   uint32_t sb = SP3_INF;
   int32_t W = 0;  // -v (this thread's column)
   int path = -1, pos = -1, r4c = -1;
   uint32_t lo = ~0u;  // key tie-break bits; ~0: left `remaining` (or j >= n)
-  uint32_t accm = 0, acca = 0;
+  uint32_t accU = 0, accW = 0;  // OR of every checked u~ + CU, W + CW (LatticeRange)
   int steps = 0;
   uint64_t tA = 0, tB = 0, tC = 0, tD = 0, ts = 0;
   auto stamp = [&](uint64_t &acc) {
@@ -836,8 +871,7 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
         asm volatile("" ::"v"(c), "s"(ui));
         stamp(tA);
       }
-      accm = max(accm, (uint32_t)(ui + mU) & 511u);
-      acca = max(acca, (uint32_t)(ui < 0 ? -ui : ui));
+      accU |= (uint32_t)ui + LR.CU;
       uint32_t bse = (uint32_t)(SP3_BIAS - ui);
       asm volatile("" : "+s"(bse));
       // (a removed column never improves: r >= minVal >= its spc; a column
@@ -907,7 +941,7 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
       if (r4c >= 0) u32[r4c] += d;
       S.path[j] = (int16_t)path;
     }
-    big |= !sp3_in_range(W, 500, mW);
+    accW |= (uint32_t)W + LR.CW;
     if (tid == 0) u32[cur] += minVal;
     __syncthreads();
     if (tid == 0) {  // augment along the path from the sink back to cur
@@ -930,8 +964,8 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
     seg[2] = tC;
     seg[3] = tD;
   }
-  big |= accm > (uint32_t)(2 * mU) || acca > (uint32_t)(1000 * 512 + mU);
-  if (colv) big |= !sp3_in_range(u32[j], 1000, mU);
+  big |= ((accU & LR.MU) | (accW & LR.MW)) != 0;
+  if (colv) big |= (((uint32_t)u32[j] + LR.CU) & LR.MU) != 0;  // (the output decode's u)
   steps_out = steps;
   return __syncthreads_or(big) != 0;
 }
@@ -968,16 +1002,16 @@ constexpr int TWIN_LUT = 1024;  // 3 classes x 256, padded to the 10-bit index m
 // code pair (c1 | c2 << 8), so that a Dijkstra step decodes its cost with a
 // few VALU instead of a dependent LDS table read (round 2's cost table):
 //   a (8 bits) | k (5) << 8 | up (1) << 13 | dbl (1) << 14,
-//   m = ((E & -2^k) + up * 2^k) << dbl,   cost = -a * 2^32 + m   (units).
+//   m = ((E >> (k - dbl)) + up) << k,   cost = -a * 2^32 + m   (units).
 // One hit (cls 1): k, up reproduce one_hit_residual(a, E) (E rounded to 2^k,
 // the rounding direction precomputed); both wish (cls 2): k = 31, m = 0;
-// neither (cls 0): k = 0, dbl, m = 2E.  a = a1 + a2 (wish values).  The
+// neither (cls 0): k = 1, dbl, m = 2E.  a = a1 + a2 (wish values).  The
 // context checks the decode against twin_cost's arithmetic for every pair.
 __host__ __device__ __forceinline__ uint32_t twin_entry(uint32_t code16, int nw1, int64_t E) {
   const uint32_t c1 = code16 & 0xFFu, c2 = code16 >> 8;
   const uint32_t a = (c1 ? nw1 - c1 : 0u) + (c2 ? nw1 - c2 : 0u);
   if (c1 && c2) return a | (31u << 8);
-  if (!(c1 | c2)) return 1u << 14;
+  if (!(c1 | c2)) return (1u << 8) | (1u << 14);  // (k = 1, dbl: m = E << 1)
   const int k = 39 - __builtin_clz(2u * a - 1u);  // (p + 8 of one_hit_residual)
   const int64_t q = (int64_t)1 << k;
   const int64_t rem = E & (q - 1), base = E - rem, half = q >> 1;
@@ -986,10 +1020,18 @@ __host__ __device__ __forceinline__ uint32_t twin_entry(uint32_t code16, int nw1
 }
 template <int SH>
 __host__ __device__ __forceinline__ int64_t twin_entry_cost(uint32_t e, uint32_t E32) {
-  const uint32_t a = e & 0xFFu, k = (e >> 8) & 31u, up = (e >> 13) & 1u, dbl = (e >> 14) & 1u;
-  const uint32_t q = 1u << k;
-  const uint32_t m = ((E32 & (0u - q)) + up * q) << dbl;
-  return (int64_t)(((uint64_t)m << SH) - ((uint64_t)a << (32 + SH)));
+  // m = ((E >> (k - dbl)) + up) << k: E rounded to a multiple of 2^k (up:
+  // the float32 sum rounded up; k = 31: both wish, m = 0) or, for a miss pair
+  // (dbl, k = 1), 2E -- ((E & -2^k) + up * 2^k) << dbl of round 3 in fewer
+  // VALU: t = e >> 8 holds k in its low 5 bits, which the shifts use directly
+  const uint32_t a = e & 0xFFu, t = e >> 8, up = (t >> 5) & 1u, dbl = (t >> 6) & 1u;
+  const uint32_t m = ((E32 >> ((t - dbl) & 31u)) + up) << (t & 31u);
+  if constexpr (SH == 0) {
+    return (int64_t)((uint64_t)m - ((uint64_t)a << 32));
+  } else {  // (the two 32-bit halves of (m - a * 2^32) << SH)
+    const uint32_t lo = m << SH, hi = (m >> (32 - SH)) - (a << SH);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  }
 }
 // child-side happiness of both twins: 2a (both wish), 2a - 1 (one), -2 (none)
 __device__ __forceinline__ int64_t twin_entry_happy(uint32_t e) {
@@ -1124,7 +1166,7 @@ __host__ __device__ __forceinline__ SantaLds santa_lds_layout(int n, int mode, i
   L.c4r = off;   off += r16((size_t)n * 2);
   L.r4c = off;   off += r16((size_t)n * 2);
   L.path = off;  off += r16((size_t)n * 2);
-  L.red = off;   off += r16((size_t)4 * SANTA_NW * 8);
+  L.red = off;   off += r16((size_t)(4 * SANTA_NW > SC_RING ? 4 * SANTA_NW : SC_RING) * 8);
   L.head = off;  off += r16((size_t)ng * 4);
   L.nxt = off;   off += r16((size_t)n * 2);
   L.part = off;  off += r16((size_t)SANTA_NW * 3 * 8);
@@ -2747,11 +2789,12 @@ __device__ __forceinline__ uint32_t tile2_get(const u32x32 &T0, const u32x32 &T1
 // slot; the winner's row comes from a packed byte per column (one readlane).
 // Exactness is checked, not assumed: every row dual a step reads (u~, a
 // scalar) and every column dual after its update (W = -v) stays within
-// |A| <= 1000 / 500 and |m| <= 2M/3 / M/3, which bounds every relaxation value
-// by |A| <= 1627 (inside the 21-bit key field) and |m| <= M; a block that
-// leaves the range is left untouched for the fallback launch (never on the
-// synthetic Kaggle-shaped rounds, where m stays 0 on every dual:
-// tools/analysis/mrange.py; forced in the tests by SH_FLAG_TEST_RANGE).
+// |A| < 1024 / 512 and |m| <= 2^bU / 2^cW (LatticeRange), which bounds every
+// relaxation value by |A| < 1662 (inside the 21-bit key field) and |m| <= M;
+// a block that leaves the range is left untouched for the fallback launch
+// (never on the synthetic Kaggle-shaped rounds, where m stays 0 on every dual
+// and |A| <= 100: tools/analysis/mrange.py; forced in the tests by
+// SH_FLAG_TEST_RANGE).
 // Per step: ~70 VALU (round 2's 64-bit santa_sp2_kernel: 108), no 64-bit LDS traffic.
 // ---------------------------------------------------------------------------
 // TIMED (SH_FLAG_TIMING, dev): shader-clock cycles per segment of the solve,
@@ -2814,7 +2857,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   *(int4 *)(rowc + 4 * lane) = make_int4(1, 1, 1, 1);  // every slot a miss (V = 1)
   // the lattice bound M (2M * E < 2^32, at most 199 so that |m| fits the packing)
   const int Mm = (int)min((int64_t)199, (int64_t)(0xFFFFFFFFll / E) / 2);
-  const int mW = (Mm - 1) / 3, mU = Mm - 1 - mW;  // |m(W)| + |m(u~)| + 1 <= M
+  const LatticeRange LR(Mm);  // |m(W)| + |m(u~)| + 1 <= M, as OR-accumulated bit tests
   __syncthreads();
   __builtin_amdgcn_s_setprio(3);  // (lowered over the last Dijkstras, below)
   uint64_t tA = 0, tB = 0, tC = 0, tD = 0, tA1 = 0, ts = 0;
@@ -2847,8 +2890,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   // the lattice range left (per-lane flag); SH_FLAG_TEST_RANGE and
   // SH_FLAG_EXACT_ARGMIN send every block to the fallback launch (the
   // windowed-key solver, whose two-pass argmin the latter selects)
-  bool bad = (a.flags & (SH_FLAG_TEST_RANGE | SH_FLAG_EXACT_ARGMIN)) != 0;
-  uint32_t accm = 0, acca = 0;                     // range of every u~ a step read (see below)
+  bool bad = (a.flags & (SH_FLAG_TEST_RANGE | SH_FLAG_EXACT_ARGMIN)) != 0 || !LR.ok;
+  uint32_t accU = 0;  // OR of u~ + CU over every step (SGPR), see LatticeRange
+  uint32_t accW = 0;  // OR of W + CW over every Dijkstra (this lane's columns)
   const int l4 = 4 * lane;
   int colk[4];  // this lane's columns (VGPR constants for the book-keeping compares)
 #pragma unroll
@@ -2988,9 +3032,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const int32_t cc[4] = {c01.x, c01.y, c23.x, c23.y};
         // u~[i] = u[i] - minVal (row i is reached at the current minimum)
         const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
-        // range of u~ (scalar): the largest m + mU field and the largest |V|
-        accm = max(accm, (uint32_t)(ui + mU) & 511u);
-        acca = max(acca, (uint32_t)(ui < 0 ? -ui : ui));
+        accU |= (uint32_t)ui + LR.CU;  // (the range of u~, scalar: two SALU)
         if constexpr (TIMED) {
           asm volatile("" ::"v"(cc[0]), "v"(cc[3]), "s"(ui));
           stamp(tA);
@@ -3043,7 +3085,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
         const int32_t dd = vk ? (int32_t)(mvb - sb[k]) : 0;
         W[k] += dd;
-        bad |= !sp3_in_range(W[k], 500, mW);
+        accW |= (uint32_t)W[k] + LR.CW;
         const int ua = vk ? (int)((r4c >> (8 * k)) & 0xFFu) : 256 + lane;
         __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -3077,10 +3119,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   __syncthreads();
 
   {  // the lattice range (see above): leave the block to the fallback launch
-    bool big = bad || accm > (uint32_t)(2 * mU) || acca > (uint32_t)(1000 * 512 + mU);
+    bool big = bad || ((accU & LR.MU) | (accW & LR.MW)) != 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (4 * lane + k < n) big |= !sp3_in_range(u_l[4 * lane + k], 1000, mU);
+    for (int k = 0; k < 4; ++k)  // (the output decode's u)
+      if (4 * lane + k < n) big |= (((uint32_t)u_l[4 * lane + k] + LR.CU) & LR.MU) != 0;
     if (__builtin_expect(__any(big), 0)) {
       if (lane == 0) {
         const int p = atomicAdd(a.ovf_cnt, 1);

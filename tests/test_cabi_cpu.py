@@ -88,6 +88,17 @@ def test_ctx_create_rejects_invalid_tables_without_gpu():
     assert _ctx_create(sd.wish, sd.goodkids, 0, sd.ng, sd.nq) == _lib.SH_ERR_ARGS
 
 
+@pytest.mark.parametrize("n_wish", [10, 100])
+def test_ctx_create_host_checks_pass_without_gpu(n_wish):
+    """Valid tables pass every host-side check of sh_ctx_create -- including
+    the C++ twins tile-entry decode against the float32 pair sums for every
+    code pair -- and only the first device call fails here (no GPU): the
+    error is SH_ERR_HIP, not SH_ERR_ARGS."""
+    sd = D.synthetic(seed=1, nc=20000, ng=200, nq=100, n_wish=n_wish, n_good=100)
+    rc = _ctx_create(sd.wish, sd.goodkids, sd.nc, sd.ng, sd.nq)
+    assert rc == _lib.SH_ERR_HIP, (rc, _lib.last_error())
+
+
 @pytest.mark.parametrize("count", [1, 2, 3, 17, 1000, 19968, 954880])
 def test_feistel_is_a_bijection(count):
     f = S.Feistel(123, 4, count)

@@ -19,7 +19,7 @@ def entry(c1: int, c2: int, n_wish: int, E: int) -> int:
     if c1 and c2:
         return a | (31 << 8)
     if not (c1 or c2):
-        return 1 << 14
+        return (1 << 8) | (1 << 14)  # k = 1 with the double bit: m = E << 1 (round 4)
     k = 39 - (32 - (2 * a - 1).bit_length())  # 39 - clz32(2a - 1)
     q = 1 << k
     rem, half = E & (q - 1), q >> 1
@@ -29,7 +29,30 @@ def entry(c1: int, c2: int, n_wish: int, E: int) -> int:
 
 
 def decode(e: int, E: int) -> int:
+    """twin_entry_cost<0> (round 4): m = ((E >> (k - dbl)) + up) << k."""
+    a, t = e & 0xFF, e >> 8
+    up, dbl = (t >> 5) & 1, (t >> 6) & 1
+    m = (((E >> ((t - dbl) & 31)) + up) << (t & 31)) & 0xFFFFFFFF
+    return m - (a << 32)
+
+
+def decode_scaled(e: int, E: int, sh: int = 17) -> int:
+    """twin_entry_cost<17>: the two 32-bit halves of (m - a * 2^32) << sh."""
+    a, t = e & 0xFF, e >> 8
+    up, dbl = (t >> 5) & 1, (t >> 6) & 1
+    m = (((E >> ((t - dbl) & 31)) + up) << (t & 31)) & 0xFFFFFFFF
+    lo = (m << sh) & 0xFFFFFFFF
+    hi = ((m >> (32 - sh)) - (a << sh)) & 0xFFFFFFFF
+    v = (hi << 32) | lo
+    return v - (1 << 64) if v >> 63 else v
+
+
+def decode_r3(e: int, E: int) -> int:
+    """Round 3's form of the same decode: ((E & -2^k) + up * 2^k) << dbl
+    (a miss pair then had k = 0)."""
     a, k, up, dbl = e & 0xFF, (e >> 8) & 31, (e >> 13) & 1, (e >> 14) & 1
+    if dbl:
+        k = 0
     q = (1 << k) & 0xFFFFFFFF
     m = (((E & ((0 - q) & 0xFFFFFFFF)) + up * q) << dbl) & 0xFFFFFFFF
     return m - (a << 32)
@@ -47,3 +70,5 @@ def test_twin_entries_decode_to_float32_sums(n_wish):
             e = entry(c1, c2, n_wish, E)
             assert e < 1 << 16
             assert decode(e, E) == want, (n_wish, c1, c2)
+            assert decode_r3(e, E) == want, (n_wish, c1, c2)
+            assert decode_scaled(e, E) == want * (1 << 17), (n_wish, c1, c2)

@@ -5,6 +5,8 @@
  * value has |m| <= 199, comparing the packed pairs A * K + m (K >= 400)
  * lexicographically makes exactly the decisions of the int64 solve.
  *   mrange_block(n, C, out[4]) -> out = {max|m| over u, v, spc/r, minVal}
+ *   mrange_block_a(n, C, out[4], outa[4]) -> also outa = max|A| of the same
+ *   values (A = the 2^32 component, a wish of rank r is A = -(100 - r))
  * returns the number of values that do not decompose with |m| < 400. */
 #include <stdint.h>
 #include <stdlib.h>
@@ -20,7 +22,14 @@ static int mof(int64_t x, int *bad) {
   ++*bad;
   return 0;
 }
-#define UPD(slot, x) do { int mm = mof((x), &bad); if (mm < 0) mm = -mm; if (mm > out[slot]) out[slot] = mm; } while (0)
+#define UPD(slot, x) do { int64_t xx_ = (x); int mm = mof(xx_, &bad); \
+    int64_t aa = (xx_ - (int64_t)mm * E) >> 32; if (aa < 0) aa = -aa; \
+    if (mm < 0) mm = -mm; if (mm > out[slot]) out[slot] = mm; \
+    if (out8 && aa > out8[slot]) out8[slot] = (int)aa; } while (0)
+
+static int *out8 = 0;  /* optional: max |A| (the 2^32 component) per slot */
+
+int mrange_block_a(int n, const int64_t *C, int *out, int *outa);
 
 int mrange_block(int n, const int64_t *C, int *out) {
   int64_t *u = calloc(n, 8), *v = calloc(n, 8), *spc = malloc(n * 8);
@@ -64,4 +73,12 @@ int mrange_block(int n, const int64_t *C, int *out) {
   }
   free(u); free(v); free(spc); free(path); free(c4r); free(r4c); free(rem); free(SR); free(SC);
   return bad;
+}
+
+int mrange_block_a(int n, const int64_t *C, int *out, int *outa) {
+  outa[0] = outa[1] = outa[2] = outa[3] = 0;
+  out8 = outa;
+  int b = mrange_block(n, C, out);
+  out8 = 0;
+  return b;
 }

@@ -20,7 +20,7 @@ so = "/tmp/libmrange.so"
 subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(os.path.dirname(__file__), "mrange.c")],
                check=True)
 L = ctypes.CDLL(so)
-L.mrange_block.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+L.mrange_block_a.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 per = int(sys.argv[3]) if len(sys.argv) > 3 else 64
@@ -29,24 +29,30 @@ tri, tw = sd.families
 lo, count, nb = single_geometry(sd.nc, n, tri, tw)
 t = sd.types.copy()
 worst = np.zeros(4, dtype=np.int32)
+worsta = np.zeros(4, dtype=np.int32)
 for rnd in range(rounds):
     rows = sample_blocks(2017, rnd, lo, count, 1, n, nb)
     pick = np.random.default_rng(rnd).choice(nb, min(per, nb), replace=False)
     mx = np.zeros(4, dtype=np.int32)
+    mxa = np.zeros(4, dtype=np.int32)
     bad = 0
 
     def one(b):
         C = oracle.cost_single(sd.wish, t, rows[b], ng=sd.ng)
         out = np.zeros(4, dtype=np.int32)
-        nb_ = L.mrange_block(n, C.ctypes.data, out.ctypes.data)
-        return out, nb_
+        outa = np.zeros(4, dtype=np.int32)
+        nb_ = L.mrange_block_a(n, C.ctypes.data, out.ctypes.data, outa.ctypes.data)
+        return out, outa, nb_
 
     with cf.ThreadPoolExecutor(8) as ex:
-        for out, b_ in ex.map(one, pick):
+        for out, outa, b_ in ex.map(one, pick):
             mx = np.maximum(mx, out)
+            mxa = np.maximum(mxa, outa)
             bad += b_
     worst = np.maximum(worst, mx)
-    print(f"round {rnd}: max|m| u {mx[0]} v {mx[1]} r {mx[2]} minVal {mx[3]}  undecodable {bad}", flush=True)
+    worsta = np.maximum(worsta, mxa)
+    print(f"round {rnd}: max|m| u {mx[0]} v {mx[1]} r {mx[2]} minVal {mx[3]}; max|A| u {mxa[0]} v {mxa[1]} "
+          f"r {mxa[2]} minVal {mxa[3]}  undecodable {bad}", flush=True)
     chunks = [rows[i:i + 64] for i in range(0, nb, 64)]
     with cf.ThreadPoolExecutor(8) as ex:
         list(ex.map(lambda ch: oracle.round_blocks(0, sd.wish, t, ch, ng=sd.ng), chunks))

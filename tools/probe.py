@@ -101,6 +101,8 @@ def main():
         out["segments_cycles_per_step_maxblock"] = {nm: float(cv[imax, q] / sv[imax])
                                                     for q, nm in enumerate(names)}
     out["blocks"] = B
+    out["n"] = a.n
+    out["mode"] = a.mode
     out["budget"] = a.budget
     out["cap"] = cap
     out["flags"] = a.flags

@@ -12,10 +12,11 @@
 set -e
 TAG=${1:-r03s8}
 BLOCKS=${2:-467}
+EXTRA=${3:-}   # more probe arguments, e.g. "--n 2000" (the reference's block size)
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-P="python3 -u tools/probe.py --phase solve --reps 1 --blocks $BLOCKS"
+P="python3 -u tools/probe.py --phase solve --reps 1 --blocks $BLOCKS $EXTRA"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT -o trace --output-format csv -- $P > $OUT/probe_trace.json
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT -o fetch --output-format csv -- $P > $OUT/probe_fetch.json
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT -o write --output-format csv -- $P > $OUT/probe_write.json
