@@ -765,7 +765,16 @@ constexpr int SP3_SH = 11;                  // key tie-break field: class 1 | pk
 constexpr int32_t SP3_BIAS = 1 << 20;       // spc_V + BIAS in [0, 2^21) (key field)
 constexpr uint32_t SP3_INF = (1u << 21) - 1u;  // "infinite" spc (never a live winner)
 
-// The lattice range as OR-accumulated bit tests (round 4): a value V passes
+// V = A * 512 + m with |A| <= amax and |m| <= mmax (2 * mmax < 512)
+__device__ __forceinline__ bool sp3_in_range(int32_t V, int amax, int mmax) {
+  return (((uint32_t)(V + mmax) & 511u) <= (uint32_t)(2 * mmax)) &&
+         ((uint32_t)(V + amax * 512 + mmax) <= (uint32_t)(2 * (amax * 512 + mmax)));
+}
+
+// The lattice range as OR-accumulated bit tests (round 4, santa_sp3_kernel;
+// the 4-wave solver keeps two running maxima, whose SALU fill its DPP
+// chain's wait states -- with the bit tests it ran 3 % slower,
+// profiles/r04_ab_r4b.jsonl): a value V passes
 // when t = V + C has no bit of MASK set, i.e. t < 2^H (|A| < 2^(H - 10)) and
 // (m + 2^b - 1) mod 512 < 2^(b + 1) (m in [1 - 2^b, 2^b]); OR-ing the t of
 // every value and testing once at the end checks them all -- two SALU per
@@ -814,14 +823,13 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
   const bool colv = j < n;
   int32_t *u32 = (int32_t *)S.u;
   const int Mm = (int)min((int64_t)199, (int64_t)(0xFFFFFFFFll / E) / 2);
-  const LatticeRange LR(Mm);
-  big |= !LR.ok;
+  const int mW = (Mm - 1) / 3, mU = Mm - 1 - mW;
   const uint32_t wa = lds_addr(S.red);  // the step word (LDS byte address)
   uint32_t sb = SP3_INF;
   int32_t W = 0;  // -v (this thread's column)
   int path = -1, pos = -1, r4c = -1;
   uint32_t lo = ~0u;  // key tie-break bits; ~0: left `remaining` (or j >= n)
-  uint32_t accU = 0, accW = 0;  // OR of every checked u~ + CU, W + CW (LatticeRange)
+  uint32_t accm = 0, acca = 0;
   int steps = 0;
   uint64_t tA = 0, tB = 0, tC = 0, tD = 0, ts = 0;
   auto stamp = [&](uint64_t &acc) {
@@ -871,7 +879,8 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
         asm volatile("" ::"v"(c), "s"(ui));
         stamp(tA);
       }
-      accU |= (uint32_t)ui + LR.CU;
+      accm = max(accm, (uint32_t)(ui + mU) & 511u);
+      acca = max(acca, (uint32_t)(ui < 0 ? -ui : ui));
       uint32_t bse = (uint32_t)(SP3_BIAS - ui);
       asm volatile("" : "+s"(bse));
       // (a removed column never improves: r >= minVal >= its spc; a column
@@ -941,7 +950,7 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
       if (r4c >= 0) u32[r4c] += d;
       S.path[j] = (int16_t)path;
     }
-    accW |= (uint32_t)W + LR.CW;
+    big |= !sp3_in_range(W, 500, mW);
     if (tid == 0) u32[cur] += minVal;
     __syncthreads();
     if (tid == 0) {  // augment along the path from the sink back to cur
@@ -964,8 +973,8 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
     seg[2] = tC;
     seg[3] = tD;
   }
-  big |= ((accU & LR.MU) | (accW & LR.MW)) != 0;
-  if (colv) big |= (((uint32_t)u32[j] + LR.CU) & LR.MU) != 0;  // (the output decode's u)
+  big |= accm > (uint32_t)(2 * mU) || acca > (uint32_t)(1000 * 512 + mU);
+  if (colv) big |= !sp3_in_range(u32[j], 1000, mU);
   steps_out = steps;
   return __syncthreads_or(big) != 0;
 }

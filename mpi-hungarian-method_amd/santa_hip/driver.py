@@ -180,6 +180,9 @@ class _Sums:
 
     def buffer(self, k: int):
         d = self.bufs[k]
+        zeroed = getattr(self.engine, "zeroed_delta", None)
+        if zeroed is not None:  # (GPUEngine: zeroed ahead of time, off the round's stream)
+            return zeroed(d)
         d.zero_()
         return d
 
@@ -419,16 +422,74 @@ def assert_disjoint(rows: torch.Tensor, mode: int) -> None:
 
 
 class GPUEngine:
-    """Adapter of SantaGPU to the run_rounds engine protocol."""
+    """Adapter of SantaGPU to the run_rounds engine protocol.
+
+    Two pieces of a round's bookkeeping run on a side stream, off the round's
+    critical path (round 4; each was a launch of its own between two rounds'
+    block kernels: profiles/r03e_kernel_stats.csv):
+      * sampling: round r + 1's blocks depend only on (seed, round r + 1)
+        (A1), so they are sampled while round r solves, into the other of two
+        buffers, after everything that still reads that buffer (round r - 1)
+        was enqueued (sample_kernel, ~10 us per round);
+      * the delta sums' zeroing: a buffer is zeroed right after its host copy
+        was enqueued, ready for its next round (a 16-byte fill, ~4 us)."""
 
     def __init__(self, ctx):
         self.ctx = ctx
+        self._pf_key = None
+        self._zero_ev = {}
 
     def geometry(self, mode, n):
         return self.ctx.geometry(mode, n)
 
+    def _side_stream(self):
+        if not hasattr(self, "_side"):
+            self._side = torch.cuda.Stream(self.ctx.device)
+        return self._side
+
     def sample_blocks(self, mode, n, B, seed, rnd):
-        return self.ctx.sample_blocks(mode, n, B, seed, rnd)
+        """Round rnd's block rows (A1), prefetched while round rnd - 1 solved
+        when the rounds come in order; round rnd + 1's are started on the side
+        stream.  The returned buffer stays valid until round rnd + 2 is asked
+        for (run_rounds uses it within its round)."""
+        dev = self.ctx.device
+        key = (mode, n, B, seed)
+        if self._pf_key != key:
+            self._pf_key = key
+            self._pf_buf = [torch.empty(B * n, dtype=torch.int32, device=dev) for _ in range(2)]
+            self._pf_rnd = [None, None]
+            self._pf_ev = [None, None]
+        main = torch.cuda.current_stream(dev)
+        k = rnd & 1
+        if self._pf_ev[k] is not None:  # (a prefetch into buffer k: wait for it)
+            main.wait_event(self._pf_ev[k])
+            self._pf_ev[k] = None
+        if self._pf_rnd[k] != rnd:
+            self.ctx.sample_blocks(mode, n, B, seed, rnd, out=self._pf_buf[k])
+            self._pf_rnd[k] = rnd
+        j = k ^ 1
+        if self._pf_rnd[j] != rnd + 1:
+            free = torch.cuda.Event()
+            free.record(main)  # (round rnd - 1, the last reader of buffer j, is enqueued)
+            side = self._side_stream()
+            with torch.cuda.stream(side):
+                side.wait_event(free)
+                self.ctx.sample_blocks(mode, n, B, seed, rnd + 1, out=self._pf_buf[j])
+                ev = torch.cuda.Event()
+                ev.record(side)
+            self._pf_rnd[j] = rnd + 1
+            self._pf_ev[j] = ev
+        return self._pf_buf[k]
+
+    def zeroed_delta(self, d):
+        """d, zeroed: by the side stream after its previous round's host copy
+        (delta_begin), or here on the current stream the first time."""
+        ev = self._zero_ev.pop(d.data_ptr(), None)
+        if ev is None:
+            d.zero_()
+        else:
+            torch.cuda.current_stream(d.device).wait_event(ev)
+        return d
 
     def solve_blocks(self, mode, rows, n, types, delta=None):
         self.ctx.solve_blocks(mode, rows, n, types, delta=delta)
@@ -461,9 +522,9 @@ class GPUEngine:
         return self._begin(types, d, full)
 
     def _begin(self, types, d, full: bool):
-        if not hasattr(self, "_side"):
+        if not hasattr(self, "_snaps"):
             dev = types.device
-            self._side = torch.cuda.Stream(dev)
+            self._side_stream()
             self._snaps = [torch.empty_like(types) for _ in range(2)]
             self._sums = [torch.zeros(4, dtype=torch.int64, device=dev) for _ in range(2)]
             self._host = [torch.zeros(4, dtype=torch.int64).pin_memory() for _ in range(2)]
@@ -483,14 +544,21 @@ class GPUEngine:
         ready = torch.cuda.Event()
         ready.record(main)
         done = ready
+        side = self._side
         if full:
-            side = self._side
             with torch.cuda.stream(side):
                 side.wait_event(ready)
                 self.ctx.score_sums_async(snap, out=self._sums[k])
                 self._host[k].copy_(self._sums[k], non_blocking=True)
                 done = torch.cuda.Event()
                 done.record(side)
+        if d is not None:  # zero d for its next round once its host copy is enqueued
+            with torch.cuda.stream(side):
+                side.wait_event(ready)
+                d.zero_()
+                z = torch.cuda.Event()
+                z.record(side)
+            self._zero_ev[d.data_ptr()] = z
         self._done[k] = done
         host = self._host[k]
 

@@ -13,9 +13,12 @@ case ${1:-1} in
     bash tools/profile_round.sh $TAG single > gpurun_out/prof_$TAG.log 2>&1 || exit 1
     bash tools/profile_round.sh ${TAG}t twins > gpurun_out/prof_${TAG}t.log 2>&1 || exit 1
     bash tools/profile_shards.sh ${TAG}s || exit 1
+    # the reference's own block sizes: 477 blocks of n = 2000, 6 of 3000 pairs
+    bash tools/profile_shard.sh ${TAG}n 477 "--n 2000" > gpurun_out/prof_${TAG}n.log 2>&1 || exit 1
+    bash tools/profile_shard.sh ${TAG}w 6 "--mode 1 --n 3000" > gpurun_out/prof_${TAG}w.log 2>&1 || exit 1
     ;;
   2)
-    bash tools/gpu_run.sh bench bench_twins bench_triplets bench_n2000 > gpurun_out/final_bench.log 2>&1 || exit 1
+    bash tools/gpu_run.sh bench bench_twins bench_triplets bench_n2000cpu bench_twins3000 > gpurun_out/final_bench.log 2>&1 || exit 1
     bash tools/shard_probe.sh > gpurun_out/shard_probe.log 2>&1 || exit 1
     ;;
 esac

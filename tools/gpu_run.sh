@@ -30,6 +30,8 @@ for s in "$@"; do
     bench_twins) step bench_twins 600 python -u bench.py --mode twins ;;
     bench_triplets) step bench_triplets 600 python -u bench.py --mode triplets ;;
     bench_n2000) step bench_n2000 600 python -u bench.py --n 2000 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    bench_n2000cpu) step bench_n2000cpu 900 python -u bench.py --n 2000 --steps 5 --warmup 1 --b1-seconds 20 ;;
+    bench_twins3000) step bench_twins3000 900 python -u bench.py --mode twins --n 3000 --steps 5 --warmup 1 --b1-seconds 30 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
