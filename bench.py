@@ -283,9 +283,11 @@ def scipy_baseline(sd, mode, n, seconds, ncores, rows, lo, count, stride, nb):
 
 # --------------------------------------------------------------------------- HBM traffic
 def design_kernels(kname: str):
-    """The kernels one solve launch of a design runs (the register-tile sparse
-    design builds its tiles in santa_tile_kernel, then solves in santa_sp3_kernel;
-    the events around the solve bracket both)."""
+    """The kernels one solve launch of a design may run: the register-tile
+    sparse design builds its tiles in santa_sp3_kernel itself (packed
+    wishlists, round 4) or in santa_tile_kernel first (other wishlist shapes);
+    the events around the solve bracket both.  stored_traffic sums the ones
+    the profile saw."""
     k = kname.split(" ")[0].split("<")[0]
     return ["santa_tile_kernel", k] if k == "santa_sp3_kernel" else [k]
 
@@ -337,6 +339,8 @@ def stored_traffic(knames, blocks: int, n: int = 256, mode: int = 0):
         if s.get("source_sha16") != src or not _same_launch(s, blocks, n, mode):
             continue
         hb = s.get("hbm_bytes_per_launch", {})
+        # the kernels this launch ran (the last named is the design's main kernel)
+        knames = [k for k in knames[:-1] if k in hb] + knames[-1:]
         es = [hb.get(k, {}) for k in knames]
         if all("FETCH_SIZE_bytes" in e and "WRITE_SIZE_bytes" in e for e in es):
             cal = json.load(open(calib[-1])) if calib else {}

@@ -2819,26 +2819,77 @@ __device__ __forceinline__ uint32_t tile2_get(const u32x32 &T0, const u32x32 &T1
 // round (profiles/r02g_setprio_ab.jsonl), re-checked on this kernel against
 // (64, 16, 4), (16, 4, 1) and none (profiles/r03_sp3_prio_ab.jsonl).
 constexpr int SP3_PRIO_A = 32, SP3_PRIO_B = 8, SP3_PRIO_C = 2;
-template <bool TIMED>
+
+// santa_sp3_kernel's LDS (static: every address is a constant offset).
+// Record design (santa_tile_kernel builds the tile, FUSED = false):
+struct Sp3LdsRecord {
+  int32_t rowc[256 + 32];     // current row C_V per slot + dumps
+  int32_t u_l[256 + 64];      // row duals V + a dump slot per lane
+  uint32_t ovfr[256];         // overflow range per row: start | count << 16
+  uint16_t ovf[SP2_OVF_CAP];  // overflow entries
+  int16_t ctype[256];         // column gift types (old)
+  uint8_t own[256];           // code(i, i): row i's own gift
+  uint8_t rem[256];           // scipy's `remaining`
+};
+// Fused design (FUSED = true, round 4): the wave builds its own tile, so no
+// record travels through HBM (santa_tile_kernel wrote ~67 MB per round and
+// the solve read it back).  The build's scratch -- the type table, the
+// column sort and one 64-row stage -- aliases the solve's row buffer, duals
+// and `remaining`; the column types and own codes stay in registers; 10,080
+// bytes per block, so 16 blocks per CU hold a whole 3730-block round.
+constexpr int SP4_OVF_CAP = 384;   // overflow entries per block (fused design)
+constexpr int SP4_PITCH = 17;      // dwords per staged row (32 u16 entries + pad; conflict-free rows)
+constexpr int SP4_MAX_NG = 1024;   // type-table entries (the sparse design takes ng <= 1022)
+struct Sp3LdsFused {
+  uint16_t ovfr[256];              // overflow range per row: start | count << 9 (count < 128)
+  uint16_t ovf[SP4_OVF_CAP];       // overflow entries
+  union {
+    struct {
+      int32_t rowc[256 + 32];
+      int32_t u_l[256 + 64];
+      uint8_t rem[256];
+    } s;                           // solve
+    struct {
+      uint32_t thead[SP4_MAX_NG];  // counting-sort counters, then the type table
+      uint32_t stage[64 * SP4_PITCH];  // one batch of 64 rows' entries (u16), row-major
+      uint8_t csort[272];          // columns sorted by gift type (rowc slots) + pad
+      uint8_t rcnt[64];            // per staged row: entries used (<= 32), | 0x80 = marker
+      int32_t ocnt[4];             // overflow entries allocated
+    } b;                           // build
+  } u;
+};
+
+template <bool TIMED, bool FUSED>
 __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const unsigned char *rec_all) {
-  // (static LDS: every address below is a constant offset, no base register)
-  __shared__ __attribute__((aligned(16))) int32_t rowc[256 + 32];  // current row C_V per slot + dumps
-  __shared__ __attribute__((aligned(16))) int32_t u_l[256 + 64];   // row duals V + a dump slot per lane
-  __shared__ __attribute__((aligned(16))) uint32_t ovfr[256];      // overflow range per row
-  __shared__ __attribute__((aligned(16))) uint16_t ovf[SP2_OVF_CAP];  // overflow entries
-  __shared__ __attribute__((aligned(16))) int16_t ctype[256];     // column gift types (old)
-  __shared__ __attribute__((aligned(16))) uint8_t own[256];       // code(i, i): row i's own gift
-  __shared__ __attribute__((aligned(16))) uint8_t rem[256];       // scipy's `remaining`
+  using SL = std::conditional_t<FUSED, Sp3LdsFused, Sp3LdsRecord>;
+  __shared__ __attribute__((aligned(16))) SL SM;
+  int32_t *rowc, *u_l;
+  uint8_t *rem;
+  if constexpr (FUSED) {
+    rowc = SM.u.s.rowc;
+    u_l = SM.u.s.u_l;
+    rem = SM.u.s.rem;
+  } else {
+    rowc = SM.rowc;
+    u_l = SM.u_l;
+    rem = SM.rem;
+  }
+  auto ovfr = SM.ovfr;
+  auto ovf = SM.ovf;
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
   const int n = a.n;
-  const unsigned char *rec = rec_all + (size_t)b * SP2_REC;
-  if (*(const volatile int32_t *)(rec + SP2_REC_STATUS)) return;  // skipped / left to the fallback
   const int x31 = lane & 31;
-
-  // -- the tile into VGPRs (santa_tile_kernel's record), the rest to LDS ------------
   u32x32 T0, T1;
-  {
+  // FUSED: the gift types of this lane's columns (= rows) 4 lane .. 4 lane + 3
+  // as two u16 pairs, and the own codes code(i, i) of the rows this lane
+  // built (byte c: row 64 c + lane); the epilogue moves them with ds_bpermute
+  uint32_t ct01 = 0, ct23 = 0, ownb = 0;
+
+  if constexpr (!FUSED) {
+    // -- the tile into VGPRs (santa_tile_kernel's record), the rest to LDS ----------
+    const unsigned char *rec = rec_all + (size_t)b * SP2_REC;
+    if (*(const volatile int32_t *)(rec + SP2_REC_STATUS)) return;  // skipped / left to the fallback
     const uint4 *src = (const uint4 *)(rec + SP2_REC_TILE);
     const int nq4 = (n + 15) >> 4;
 #pragma unroll
@@ -2853,11 +2904,225 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
     const uint32_t *rr = (const uint32_t *)(rec + SP2_REC_OVFR);
 #pragma unroll
     for (int k = 0; k < 4; ++k) ovfr[4 * lane + k] = rr[4 * lane + k];
-    ((uint32_t *)own)[lane] = ((const uint32_t *)(rec + SP2_REC_OWN))[lane];
+    ((uint32_t *)SM.own)[lane] = ((const uint32_t *)(rec + SP2_REC_OWN))[lane];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int r = 4 * lane + k;
-      if (r < n) ctype[r] = a.types[a.rows[(size_t)b * n + r]];
+      if (r < n) SM.ctype[r] = a.types[a.rows[(size_t)b * n + r]];
+    }
+  } else {
+    // -- build the tile in this wave (santa_tile_kernel's algorithm, one wave) -------
+    // Lane l owns columns 4l .. 4l + 3 for the column sort, then builds rows
+    // 64 c + l in four batches c; a batch's entries go to a 64-row LDS stage
+    // and are transposed into T[16 c .. 16 c + 15] (static indices).
+    uint32_t *thead = SM.u.b.thead;
+    uint8_t *csort = SM.u.b.csort;
+    uint8_t *rcnt = SM.u.b.rcnt;
+    int32_t *ocnt = SM.u.b.ocnt;
+    uint16_t *stage = (uint16_t *)SM.u.b.stage;
+    int tk[4];
+    bool badr = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = 4 * lane + k;
+      const int ch = r < n ? a.rows[(size_t)b * n + r] : 0;
+      badr |= r < n && (ch < 0 || ch >= a.nc);
+      tk[k] = ch;
+    }
+    if (__any(badr)) {
+      if (lane == 0) atomicOr(a.err, SH_ERRF_ROWS);
+      return;
+    }
+    bool badt = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = 4 * lane + k;
+      tk[k] = r < n ? (int)a.types[tk[k]] : -1;  // (the types index LDS tables: range-checked)
+      badt |= r < n && (tk[k] < 0 || tk[k] >= a.ng);
+    }
+    if (__any(badt)) {
+      if (lane == 0) atomicOr(a.err, SH_ERRF_TYPE);
+      return;
+    }
+    ct01 = (uint32_t)(uint16_t)tk[0] | ((uint32_t)(uint16_t)tk[1] << 16);
+    ct23 = (uint32_t)(uint16_t)tk[2] | ((uint32_t)(uint16_t)tk[3] << 16);
+    // -- columns sorted by gift type (counting sort) ---------------------------------
+    for (int t = lane; t < a.ng; t += WAVE) thead[t] = 0u;
+    if (lane == 0) *ocnt = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tk[k] >= 0) atomicAdd(&thead[tk[k]], 1u << 16);
+    __syncthreads();
+    int big = 0;
+    {  // exclusive scan of the counts over types -> start of each type in csort
+      const int per = (a.ng + WAVE - 1) / WAVE;
+      const int t0s = lane * per, t1s = min(a.ng, t0s + per);
+      uint32_t sum = 0;
+      for (int t = t0s; t < t1s; ++t) sum += thead[t] >> 16;
+      uint32_t run = wave_incl_scan_u32(sum) - sum;
+      for (int t = t0s; t < t1s; ++t) {
+        const uint32_t h = thead[t];
+        thead[t] = h | run;  // low half: fill cursor
+        big |= (h >> 16) >= 255u;
+        run += h >> 16;
+      }
+    }
+    if (__any(big)) {  // a type with 255+ columns: leave the block to the fallback
+      if (lane == 0) {
+        const int p = atomicAdd(a.ovf_cnt, 1);
+        a.ovf_list[p] = b;
+      }
+      return;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (tk[k] >= 0) csort[atomicAdd(&thead[tk[k]], 1u) & 0xFFFFu] = (uint8_t)rowc_slot(4 * lane + k);
+    __syncthreads();
+    // per type, in place: c0 | c1 << 8 | (count <= 3 ? c2 : start in csort) << 16 | count << 24
+    for (int t = lane; t < a.ng; t += WAVE) {
+      const uint32_t h = thead[t];
+      const uint32_t c = h >> 16, e = (h & 0xFFFFu) - c;
+      const uint32_t x2 = c <= 3u ? (uint32_t)csort[e + 2] : e;
+      thead[t] = c ? ((uint32_t)csort[e] | ((uint32_t)csort[e + 1] << 8) | (x2 << 16) | (min(c, 255u) << 24))
+                   : 0u;
+    }
+    __syncthreads();
+    // -- four batches of 64 rows: pass 1 (hit count, own code), pass 2 (entries) -----
+    const int nw = a.n_wish;
+    const int ndw = (nw + 1) >> 1;
+    const int cap = a.cap;  // (SP4_OVF_CAP, or lower under a test budget)
+    bool fits = true;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int R = 64 * c + lane;
+      const bool live = R < n;
+      int child = 0, myt = -1;
+      u32x32 G;
+      if (live) {
+        child = a.rows[(size_t)b * n + R];
+        myt = a.types[child];
+      }
+      {  // the packed wishlist: gift r at bits 10 r .. 10 r + 9 of one 128-byte line
+        const uint4 *s4 = (const uint4 *)(a.wish10 + (size_t)child * 32);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint4 v = live ? s4[q] : make_uint4(0, 0, 0, 0);
+          G[4 * q] = v.x;
+          G[4 * q + 1] = v.y;
+          G[4 * q + 2] = v.z;
+          G[4 * q + 3] = v.w;
+        }
+      }
+      auto gifts4 = [&](int d, int (&g)[4]) {  // gifts 2d .. 2d + 3: bits 20d .. 20d + 39
+        const int bit = 20 * d, dw = bit >> 5, sh = bit & 31;
+        const uint32_t w0 = G[dw & 31], w1 = G[(dw + 1) & 31], w2 = G[(dw + 2) & 31];
+        const uint32_t x = __builtin_amdgcn_alignbit(w1, w0, sh);
+        const uint32_t y = __builtin_amdgcn_alignbit(w2, w1, sh);
+        g[0] = (int)(x & 1023u);
+        g[1] = (int)((x >> 10) & 1023u);
+        g[2] = (int)((x >> 20) & 1023u);
+        g[3] = (int)(__builtin_amdgcn_alignbit(y, x, 30) & 1023u);
+      };
+      int lim = 32, obase = 0;
+      if (live) {
+        uint32_t total = 0;
+        int ownc = 0;
+#pragma unroll 1
+        for (int d = 0; d < ndw; d += 2) {
+          int g[4];
+          gifts4(d, g);
+          uint32_t h[4];
+#pragma unroll
+          for (int z = 0; z < 4; ++z) h[z] = thead[g[z]];
+#pragma unroll
+          for (int z = 0; z < 4; ++z) {
+            total += h[z] >> 24;
+            ownc = (g[z] == myt) ? 2 * d + z + 1 : ownc;  // (the last occurrence, as the reference's overwrite)
+          }
+        }
+        ownb |= (uint32_t)ownc << (8 * c);
+        if (total > 32u) {  // entries 31.. to the overflow list, the marker in entry 31
+          lim = 31;
+          const int extra = (int)total - 31;
+          obase = atomicAdd(ocnt, extra);
+          if (obase + extra > cap || extra > 127) fits = false;
+        }
+        ovfr[R] = lim == 31 ? (uint16_t)(obase | ((int)(total - 31u) << 9)) : (uint16_t)0;  // (0: no overflow)
+        rcnt[lane] = (uint8_t)(total > 32u ? 0x80u | 31u : total);
+      } else {
+        rcnt[lane] = 0;
+      }
+      if (live && fits) {  // pass 2: the entries (slot | a << 9, a = n_wish - rank) in wish order
+        uint16_t *srow = stage + lane * (2 * SP4_PITCH);
+        uint16_t *orow = ovf + obase - lim;  // entry x >= lim goes to orow[x]
+        int x = 0;
+#pragma unroll 1
+        for (int d = 0; d < ndw; d += 2) {
+          int g[4];
+          gifts4(d, g);
+          uint32_t h[4];
+#pragma unroll
+          for (int z = 0; z < 4; ++z) h[z] = thead[g[z]];
+#pragma unroll
+          for (int z = 0; z < 4; ++z) {
+            const int r = 2 * d + z;
+            const uint32_t hz = h[z];
+            const uint32_t A = (uint32_t)(nw - r) << 9;
+            const int cg = (int)(hz >> 24);
+            srow[(cg >= 1 && x < lim) ? x : 32] = (uint16_t)((hz & 0xFFu) | A);
+            srow[(cg >= 2 && x + 1 < lim) ? x + 1 : 32] = (uint16_t)(((hz >> 8) & 0xFFu) | A);
+            if (__any(cg >= 3)) {
+              if (cg == 3) {
+                srow[x + 2 < lim ? x + 2 : 32] = (uint16_t)(((hz >> 16) & 0xFFu) | A);
+              } else if (cg >= 4) {  // the type's columns 2.. from csort
+                const int e = (int)((hz >> 16) & 0xFFu);
+                for (int m = 2; m < cg; ++m) srow[x + m < lim ? x + m : 32] = (uint16_t)((uint32_t)csort[e + m] | A);
+              }
+            }
+            if (__any(x + cg > lim)) {  // entries lim.. of this row to the overflow list
+              for (int m = max(lim - x, 0); m < cg; ++m) {
+                const uint32_t cc = (m < 2 || cg == 3) ? ((hz >> (8 * m)) & 0xFFu)
+                                                       : (uint32_t)csort[((hz >> 16) & 0xFFu) + m];
+                orow[x + m] = (uint16_t)(cc | A);
+              }
+            }
+            x += cg;
+          }
+        }
+      }
+      if (__any(!fits)) {  // does not fit: leave the block to the fallback kernel
+        if (lane == 0) {
+          const int p = atomicAdd(a.ovf_cnt, 1);
+          a.ovf_list[p] = b;
+        }
+        return;
+      }
+      __syncthreads();
+      // stage -> T[16 c + q]: lane 32 L + x takes entry x of batch rows 4 q + 2 L
+      // (low half) and 4 q + 2 L + 1 (high half)
+      const int L = lane >> 5;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        uint32_t dw = 0;
+#pragma unroll
+        for (int H = 0; H < 2; ++H) {
+          const int lr = 4 * q + 2 * L + H;
+          const uint32_t rc = rcnt[lr];
+          uint32_t e = 256u + (uint32_t)x31;  // unused entry: the lane's dump slot
+          if ((uint32_t)x31 < (rc & 0x7Fu))
+            e = stage[lr * (2 * SP4_PITCH) + x31];
+          else if ((rc & 0x80u) && x31 == 31)
+            e = (256u + 31u) | (SP2_MARK << 9);
+          dw |= e << (16 * H);
+        }
+        if (16 * c + q < 32)
+          T0[16 * c + q] = dw;
+        else
+          T1[16 * c + q - 32] = dw;
+      }
+      __syncthreads();  // (the next batch rewrites the stage)
     }
   }
   for (int r = lane; r < n; r += WAVE) u_l[r] = 0;
@@ -3028,7 +3293,8 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(ea == SP2_MARK) != 0, 0)) {
           rowc[sslot] = sval;
           const uint32_t rg = ovfr[i];
-          const int os = (int)(rg & 0xFFFFu), oc = (int)(rg >> 16);
+          const int os = FUSED ? (int)(rg & 0x1FFu) : (int)(rg & 0xFFFFu);
+          const int oc = FUSED ? (int)(rg >> 9) : (int)(rg >> 16);
           for (int x = lane; x < oc; x += WAVE) {
             const uint32_t e2 = ovf[os + x];
             rowc[e2 & 0x1FFu] = -(int32_t)((e2 >> 9) << 9);
@@ -3151,10 +3417,22 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
     for (int q = 0; q < 4; ++q) vq[q] = __shfl(-W[q], col >> 2, WAVE);
     const int cs = col & 3;
     const int32_t vcol = (cs == 0) ? vq[0] : (cs == 1) ? vq[1] : (cs == 2) ? vq[2] : vq[3];
+    uint32_t co;
+    int told, tnew;
+    if constexpr (FUSED) {  // (registers: own code of row i built by lane i % 64 in batch i / 64)
+      const uint32_t ob = (uint32_t)__shfl((int)ownb, i & 63, WAVE);
+      co = (ob >> (8 * (i >> 6))) & 0xFFu;
+      told = (int)(((k < 2 ? ct01 : ct23) >> (16 * (k & 1))) & 0xFFFFu);
+      const uint32_t t01 = (uint32_t)__shfl((int)ct01, col >> 2, WAVE);
+      const uint32_t t23 = (uint32_t)__shfl((int)ct23, col >> 2, WAVE);
+      tnew = (int)((((col & 2) ? t23 : t01) >> (16 * (col & 1))) & 0xFFFFu);
+    } else {
+      co = i < n ? SM.own[i] : 0u;
+      told = i < n ? SM.ctype[i] : 0;
+      tnew = i < n ? SM.ctype[col] : 0;
+    }
     if (i < n) {
-      const uint32_t co = own[i];
       const int chd = a.rows[(size_t)b * n + i];
-      const int told = ctype[i], tnew = ctype[col];
       if (a.flags & SH_FLAG_BUILD_ONLY) {
         cost += single_cost(co, nw1, E);
       } else {
@@ -4068,7 +4346,8 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
   const int cap = sp_capacity(ctx);
   const size_t lds = tile2 ? tile_lds_layout(ctx->ng).total : sp_lds_layout(ctx->ng, cap).total;
   if (lds > 64 * 1024) return fail(SH_ERR_ARGS, "sparse-tile LDS budget above 64 KiB");
-  if (tile2 && ctx->rec_cap < B) {  // per-block tile records (HBM)
+  const bool fused = tile2 && ctx->d_wish10;  // (in-kernel build: packed wishlists only)
+  if (tile2 && !fused && ctx->rec_cap < B) {  // per-block tile records (HBM)
     if (ctx->d_rec) HIP_TRY(hipFree(ctx->d_rec));
     ctx->d_rec = nullptr;
     ctx->rec_cap = 0;
@@ -4086,18 +4365,26 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
   if (tile2) {
     // overflow capacity per block; a sparse budget set for tests lowers it
     // (budget / 16 entries) so that some or all blocks take the fallback
-    a.cap = ctx->sp_budget > 0 ? std::min(SP2_OVF_CAP, ctx->sp_budget / 16) : SP2_OVF_CAP;
-    if (ctx->d_wish10)
-      hipLaunchKernelGGL(santa_tile_kernel<2>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
-    else if (vec)
-      hipLaunchKernelGGL(santa_tile_kernel<1>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
-    else
-      hipLaunchKernelGGL(santa_tile_kernel<0>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
-    HIP_TRY(hipGetLastError());
-    if (a.flags & SH_FLAG_TIMING)
-        hipLaunchKernelGGL(santa_sp3_kernel<true>, dim3(B), dim3(WAVE), 0, s, a, (const unsigned char *)ctx->d_rec);
+    const int ocap = fused ? SP4_OVF_CAP : SP2_OVF_CAP;
+    a.cap = ctx->sp_budget > 0 ? std::min(ocap, ctx->sp_budget / 16) : ocap;
+    if (fused) {  // one kernel: each wave builds its block's tile, then solves it
+      if (a.flags & SH_FLAG_TIMING)
+        hipLaunchKernelGGL((santa_sp3_kernel<true, true>), dim3(B), dim3(WAVE), 0, s, a, nullptr);
       else
-        hipLaunchKernelGGL(santa_sp3_kernel<false>, dim3(B), dim3(WAVE), 0, s, a, (const unsigned char *)ctx->d_rec);
+        hipLaunchKernelGGL((santa_sp3_kernel<false, true>), dim3(B), dim3(WAVE), 0, s, a, nullptr);
+    } else {
+      if (vec)
+        hipLaunchKernelGGL(santa_tile_kernel<1>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
+      else
+        hipLaunchKernelGGL(santa_tile_kernel<0>, dim3(B), dim3(TILE_NW * WAVE), lds, s, a, ctx->d_rec);
+      HIP_TRY(hipGetLastError());
+      if (a.flags & SH_FLAG_TIMING)
+        hipLaunchKernelGGL((santa_sp3_kernel<true, false>), dim3(B), dim3(WAVE), 0, s, a,
+                           (const unsigned char *)ctx->d_rec);
+      else
+        hipLaunchKernelGGL((santa_sp3_kernel<false, false>), dim3(B), dim3(WAVE), 0, s, a,
+                           (const unsigned char *)ctx->d_rec);
+    }
   } else if (vec)
     hipLaunchKernelGGL(santa_sp_kernel<true>, dim3(B), dim3(WAVE), lds, s, a);
   else
@@ -4218,7 +4505,9 @@ int resident_blocks(sh_ctx *ctx, int design, int mode, int n, int B) {
       return occ_blocks(ctx, santa_block_kernel<1, 1>, SANTA_WG, santa_lds_layout(n, 1, ctx->ng).total);
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
     case SH_DESIGN_VT_TILE: return vt_tile_slots(ctx);
-    case SH_DESIGN_SPARSE3: return occ_blocks(ctx, santa_sp3_kernel<false>, WAVE, 0);
+    case SH_DESIGN_SPARSE3:
+      return ctx->d_wish10 ? occ_blocks(ctx, santa_sp3_kernel<false, true>, WAVE, 0)
+                           : occ_blocks(ctx, santa_sp3_kernel<false, false>, WAVE, 0);
     default:
       return occ_blocks(ctx, santa_sp_kernel<true>, WAVE, sp_lds_layout(ctx->ng, sp_capacity(ctx)).total);
   }

@@ -47,7 +47,7 @@ SH_DESIGN_NAMES = {0: "santa_sp_kernel (1-wave sparse LDS tile)", 1: "santa_bloc
                    4: "santa_block_kernel (twins, 4-wave code-pair tile)",
                    5: "santa_big_kernel (row rebuilt from the wishlist)",
                    6: "(retired: santa_sp2_kernel)",
-                   7: "santa_sp3_kernel (1-wave sparse register tile, 32-bit lattice keys)"}
+                   7: "santa_sp3_kernel (1-wave sparse register tile built in-kernel, 32-bit lattice keys)"}
 SH_MAX_N = 1024
 SH_MAX_N_SANTA = 4096
 

@@ -23,8 +23,8 @@ LIB = os.path.join(ROOT, "mpi-hungarian-method_amd", "santa_hip", "libsanta_hip.
 # spill -- santa_tile_kernel<0>, 28 dwords, outside its loops -- are not
 # held to it)
 NO_SCRATCH = (
-    "santa_tile_kernelILi2E", "santa_tile_kernelILi1E",
-    "santa_sp3_kernelILb0E", "santa_vt_kernelILi0ELi1E", "santa_vt_kernelILi0ELi0E",
+    "santa_tile_kernelILi1E",
+    "santa_sp3_kernelILb0ELb0E", "santa_sp3_kernelILb0ELb1E", "santa_vt_kernelILi0ELi1E", "santa_vt_kernelILi0ELi0E",
     "santa_block_kernelILi1ELi0ELb0E", "santa_block_kernelILi1ELi1ELb0E",
     "santa_big_kernel", "score_kernel", "lsap_i64_kernel", "lsap_f64_kernel",
 )
