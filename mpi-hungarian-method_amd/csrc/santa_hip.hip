@@ -764,6 +764,8 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
 constexpr int SP3_SH = 11;                  // key tie-break field: class 1 | pkey 8 | k 2
 constexpr int32_t SP3_BIAS = 1 << 20;       // spc_V + BIAS in [0, 2^21) (key field)
 constexpr uint32_t SP3_INF = (1u << 21) - 1u;  // "infinite" spc (never a live winner)
+constexpr int32_t SP3_MISS = 1 << SP3_SH;          // santa_sp3_kernel: a miss (V = 1) in key units
+constexpr uint32_t SP3_KMASK = ~((1u << SP3_SH) - 1u);  // the value field of a key
 
 // V = A * 512 + m with |A| <= amax and |m| <= mmax (2 * mmax < 512)
 __device__ __forceinline__ bool sp3_in_range(int32_t V, int amax, int mmax) {
@@ -2829,7 +2831,7 @@ struct Sp3LdsRecord {
   uint16_t ovf[SP2_OVF_CAP];  // overflow entries
   int16_t ctype[256];         // column gift types (old)
   uint8_t own[256];           // code(i, i): row i's own gift
-  uint8_t rem[256];           // scipy's `remaining`
+  uint32_t rem[512];          // scipy's `remaining`, then the rows by step (see the solve)
 };
 // Fused design (FUSED = true, round 4): the wave builds its own tile, so no
 // record travels through HBM (santa_tile_kernel wrote ~67 MB per round and
@@ -2847,7 +2849,7 @@ struct Sp3LdsFused {
     struct {
       int32_t rowc[256 + 32];
       int32_t u_l[256 + 64];
-      uint8_t rem[256];
+      uint32_t rem[512];
     } s;                           // solve
     struct {
       uint32_t thead[SP4_MAX_NG];  // counting-sort counters, then the type table
@@ -2864,7 +2866,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   using SL = std::conditional_t<FUSED, Sp3LdsFused, Sp3LdsRecord>;
   __shared__ __attribute__((aligned(16))) SL SM;
   int32_t *rowc, *u_l;
-  uint8_t *rem;
+  uint32_t *rem;
   if constexpr (FUSED) {
     rowc = SM.u.s.rowc;
     u_l = SM.u.s.u_l;
@@ -3128,7 +3130,8 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   for (int r = lane; r < n; r += WAVE) u_l[r] = 0;
   const int nw1 = a.n_wish + 1;
   const int64_t E = a.E;
-  *(int4 *)(rowc + 4 * lane) = make_int4(1, 1, 1, 1);  // every slot a miss (V = 1)
+  // row values in key units (V << SP3_SH, see the solve below)
+  *(int4 *)(rowc + 4 * lane) = make_int4(SP3_MISS, SP3_MISS, SP3_MISS, SP3_MISS);  // every slot a miss
   // the lattice bound M (2M * E < 2^32, at most 199 so that |m| fits the packing)
   const int Mm = (int)min((int64_t)199, (int64_t)(0xFFFFFFFFll / E) / 2);
   const LatticeRange LR(Mm);  // |m(W)| + |m(u~)| + 1 <= M, as OR-accumulated bit tests
@@ -3144,22 +3147,33 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   };
   if constexpr (TIMED) ts = __builtin_amdgcn_s_memtime();
 
-  uint32_t sb[4];      // spc_V + BIAS (columns 4*lane + k)
-  int32_t W[4];        // -v_V
-  i32x4 path;
-  uint32_t lo[4];      // key tie-break bits; ~0: left `remaining` this Dijkstra (or j >= n)
+  // Per column 4 lane + k, in key units (a V value times 2^SP3_SH; the row
+  // values in rowc are stored so, and so is the scalar of a step):
+  //   sbp  (spc_V + BIAS) << SP3_SH | t, t the Dijkstra step (0 .. n-1) of the
+  //        column's last improvement: a later step's equal value is larger, so
+  //        one min keeps scipy's strict < and needs no compare or path select
+  //        (round 4: 3 VALU per column per step instead of 5); the path's row
+  //        is the row of step t (rowq, below); ~0: not reached
+  //   W    -v_V (the range check, the outputs), Wp = W << SP3_SH (relaxation)
+  //   lo   key tie-break bits (class << 10 | pkey << 2 | k); ~0: left
+  //        `remaining` this Dijkstra (or j >= n)
+  uint32_t sbp[4];
+  int32_t W[4], Wp[4];
+  u32x4 lo;            // (one VGPR tuple: a step's book-keeping writes lo[k] by an indexed move)
   uint32_t c4r = ~0u;  // column of row 4*lane + k in byte k
   uint32_t r4c = 0;    // row of column 4*lane + k in byte k (valid where assigned)
   uint64_t AM[4];      // assigned columns (wave masks, SGPRs)
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     W[k] = 0;
-    path[k] = -1;
+    Wp[k] = 0;
     AM[k] = 0;
   }
-  uint32_t rem0 = 0;  // rem[p] = n - 1 - p for this lane's 4 positions
-#pragma unroll
-  for (int k = 0; k < 4; ++k) rem0 |= (uint32_t)((n - 1 - (4 * lane + k)) & 0xFF) << (8 * k);
+  // rem[p]: the column at position p of scipy's `remaining`; rowq[n - 1 - t]:
+  // the LDS address of u_l[i] for the row i of step t (written by the step's
+  // LDS group from the address it reads the dual with)
+  uint32_t *rowq = rem + 256;
+  const uint32_t ubase = lds_addr(u_l);
   int steps = 0;
   // the lattice range left (per-lane flag); SH_FLAG_TEST_RANGE and
   // SH_FLAG_EXACT_ARGMIN send every block to the fallback launch (the
@@ -3167,13 +3181,6 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   bool bad = (a.flags & (SH_FLAG_TEST_RANGE | SH_FLAG_EXACT_ARGMIN)) != 0 || !LR.ok;
   uint32_t accU = 0;  // OR of u~ + CU over every step (SGPR), see LatticeRange
   uint32_t accW = 0;  // OR of W + CW over every Dijkstra (this lane's columns)
-  const int l4 = 4 * lane;
-  int colk[4];  // this lane's columns (VGPR constants for the book-keeping compares)
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    colk[k] = l4 + k;
-    asm volatile("" : "+v"(colk[k]));
-  }
   // this lane's two row-buffer words (columns 4l, 4l+1 and 4l+2, 4l+3): kept
   // in registers across the loop (recomputed per step into a register still
   // read by the pending scatter, they made the compiler wait for it)
@@ -3197,18 +3204,22 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const bool asg = __builtin_amdgcn_inverse_ballot_w64(AM[k]);
         const uint32_t pk = asg ? ((1u << 8) | pos) : (255u - pos);
         lo[k] = (j < n) ? ((pk << 2) | (uint32_t)k) : ~0u;
-        sb[k] = SP3_INF;
+        sbp[k] = ~0u;
       }
-      ((uint32_t *)rem)[lane] = rem0;
+      {
+        const int p0 = n - 1 - 4 * ln;
+        *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
+      }
       int nrem = n;
       int32_t minVal = 0;
       int i = cur;
       int sink;
-      // deferred book-keeping of the previous step: the winner (tie bits pglo,
-      // unique among the live columns) leaves `remaining`, the mover (column
-      // mv) takes its position (tie bits ^= kX)
-      uint32_t pglo = ~0u;
-      int mv = -1;
+      // deferred book-keeping of the previous step, applied in the shadow of
+      // the next step's LDS group: the winner (lane, slot) leaves `remaining`
+      // (lo = ~0), the mover (the column at the last position) takes the
+      // winner's position (its pkey bits ^= kX); a lane mask of 0: none
+      uint64_t wmask = 0, mmask = 0;
+      int kw = 0, kmv = 0;
       uint32_t kX = 0;
       bool first = true;
       for (;;) {
@@ -3221,10 +3232,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const uint32_t hl = (uint32_t)(-((i >> 1) & 1));
         const bool mine = __builtin_amdgcn_inverse_ballot_w64(((uint64_t)hl << 32) | ~hl);
         const uint32_t ea = e >> 9;
-        // expand the row: hit columns get -a * 512, the rest hold a miss (1);
-        // read this lane's four columns; put the misses back (in-order LDS)
+        // expand the row: hit columns get -a (key units), the rest hold a
+        // miss; read this lane's four columns; put the misses back (in-order LDS)
         const int sslot = mine ? (int)(e & 0x1FFu) : 256 + x31;
-        const int32_t sval = -(int32_t)(ea << 9);
+        const int32_t sval = -(int32_t)(ea << (9 + SP3_SH));
         if constexpr (TIMED) {  // (A1: the tile fetch and the entry's fields)
           asm volatile("" ::"v"(sslot), "v"(sval));
           stamp(tA1);
@@ -3234,59 +3245,41 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         int2 c01, c23;
         // The step's LDS traffic as one issue group for every row (a row with
         // more than 32 hits has the marker, whose slot is a dump slot, in its
-        // entry 31); such a row re-reads its columns below.  One path through
-        // the group keeps lo[] in one set of registers across the loop.
-        // The step's LDS traffic as one issue group: the dual and the mover,
-        // the scatter, the row reads, the un-scatter -- no wait in between
-        // (compiled, the reads waited on earlier accesses whose address
-        // registers they reused); one wait below, after the book-keeping.
-        // Operands stay live through that wait.
-        const uint32_t ua = lds_addr(u_l) + 4u * (uint32_t)i;
-        const uint32_t ra = lds_addr(rem) + (uint32_t)(nrem - 1);
+        // entry 31; such a row re-reads its columns below): the dual and the
+        // mover, the scatter, the row reads, the un-scatter, the step's row
+        // (rowq[nrem - 1] = the dual's address) -- no wait in between; then
+        // the previous step's book-keeping in their shadow, one lane and one
+        // register each (exec = that lane, the slot by GPR indexing on the lo
+        // tuple, %17 = its first register), one wait at the end.  Operands stay
+        // live through that wait.
+        const uint32_t ua = ubase + 4u * (uint32_t)i;
+        const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
         const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
-        const uint32_t one = 1;
-        // book-keeping of the previous step (as the slow path's) in the
-        // shadow of the LDS accesses, in the same asm: lo[] is updated in
-        // place (computed in C++ the new values took new registers, copied
-        // back at the loop latch), the compares write SGPR pairs read 3+
-        // instructions later (no s_nop between compare and select)
-        uint64_t t0, t1, t2, t3;
-        uint32_t x0, x1, x2, x3;
+        const int32_t miss = SP3_MISS;
+        uint64_t sv;
         asm volatile(
-            "ds_read_b32 %0, %14\n\t"
-            "ds_read_u8 %1, %15\n\t"
-            "ds_write_b32 %16, %17\n\t"
-            "ds_read2_b32 %2, %18 offset1:1\n\t"
-            "ds_read2_b32 %3, %18 offset0:128 offset1:129\n\t"
-            "ds_write_b32 %16, %19\n\t"
-            "v_cmp_ne_u32_e64 %8, %20, %4\n\t"
-            "v_cmp_ne_u32_e64 %9, %20, %5\n\t"
-            "v_cmp_ne_u32_e64 %10, %20, %6\n\t"
-            "v_cmp_ne_u32_e64 %11, %20, %7\n\t"
-            "v_cndmask_b32_e64 %4, -1, %4, %8\n\t"
-            "v_cndmask_b32_e64 %5, -1, %5, %9\n\t"
-            "v_cndmask_b32_e64 %6, -1, %6, %10\n\t"
-            "v_cndmask_b32_e64 %7, -1, %7, %11\n\t"
-            "v_cmp_eq_u32_e64 %8, %21, %23\n\t"
-            "v_cmp_eq_u32_e64 %9, %21, %24\n\t"
-            "v_cmp_eq_u32_e64 %10, %21, %25\n\t"
-            "v_cmp_eq_u32_e64 %11, %21, %26\n\t"
-            "v_cndmask_b32_e64 %12, 0, %22, %8\n\t"
-            "v_cndmask_b32_e64 %13, 0, %22, %9\n\t"
-            "v_xor_b32 %4, %4, %12\n\t"
-            "v_cndmask_b32_e64 %12, 0, %22, %10\n\t"
-            "v_xor_b32 %5, %5, %13\n\t"
-            "v_cndmask_b32_e64 %13, 0, %22, %11\n\t"
-            "v_xor_b32 %6, %6, %12\n\t"
-            "v_xor_b32 %7, %7, %13\n\t"
+            "ds_read_b32 %0, %6\n\t"
+            "ds_read_b32 %1, %7\n\t"
+            "ds_write_b32 %8, %9\n\t"
+            "ds_read2_b32 %2, %10 offset1:1\n\t"
+            "ds_read2_b32 %3, %10 offset0:128 offset1:129\n\t"
+            "ds_write_b32 %8, %11\n\t"
+            "ds_write_b32 %7, %6 offset:1024\n\t"
+            "s_mov_b64 %4, exec\n\t"
+            "s_mov_b64 exec, %12\n\t"
+            "s_set_gpr_idx_on %13, gpr_idx(DST)\n\t"
+            "v_mov_b32 %17, -1\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %14\n\t"
+            "s_set_gpr_idx_on %15, gpr_idx(SRC1,DST)\n\t"
+            "v_xor_b32 %17, %16, %17\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %4\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "+v"(lo[0]), "+v"(lo[1]),
-              "+v"(lo[2]), "+v"(lo[3]), "=&s"(t0), "=&s"(t1), "=&s"(t2), "=&s"(t3), "=&v"(x0), "=&v"(x1)
-            : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(one), "s"(pglo), "v"(mv), "v"(kX),
-              "v"(colk[0]), "v"(colk[1]), "v"(colk[2]), "v"(colk[3])
+            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "=&s"(sv), "+v"(lo)
+            : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(miss), "s"(wmask), "s"(kw), "s"(mmask),
+              "s"(kmv), "s"(kX), "v"(lo.x)
             : "memory");
-        (void)x2;
-        (void)x3;
         // (a row with more than 32 hits: the tile's entries and the overflow
         // list scattered again, the four columns re-read; the other half's
         // marker only sends a row without overflow through here, count 0)
@@ -3297,12 +3290,12 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           const int oc = FUSED ? (int)(rg >> 9) : (int)(rg >> 16);
           for (int x = lane; x < oc; x += WAVE) {
             const uint32_t e2 = ovf[os + x];
-            rowc[e2 & 0x1FFu] = -(int32_t)((e2 >> 9) << 9);
+            rowc[e2 & 0x1FFu] = -(int32_t)((e2 >> 9) << (9 + SP3_SH));
           }
           c01 = *(const int2 *)(rowc + ro0);
           c23 = *(const int2 *)(rowc + 128 + ro0);
-          rowc[sslot] = 1;
-          for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = 1;
+          rowc[sslot] = SP3_MISS;
+          for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = SP3_MISS;
         }
         const int32_t cc[4] = {c01.x, c01.y, c23.x, c23.y};
         // u~[i] = u[i] - minVal (row i is reached at the current minimum)
@@ -3312,38 +3305,41 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           asm volatile("" ::"v"(cc[0]), "v"(cc[3]), "s"(ui));
           stamp(tA);
         }
-        uint32_t bse = (uint32_t)(SP3_BIAS - ui);
-        asm volatile("" : "+s"(bse));  // (W + c + bse: one add3 per column)
+        // the step's scalar: (BIAS - u~) in key units, the step t in the low byte
+        uint32_t bse = ((uint32_t)(SP3_BIAS - ui) << SP3_SH) | (uint32_t)(n - nrem);
+        asm volatile("" : "+s"(bse));  // (Wp + c + bse: one add3 per column)
         uint32_t best = ~0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const uint32_t r = (uint32_t)W[k] + (uint32_t)cc[k] + bse;
-          // (a removed column never improves: r >= minVal >= its spc)
-          const bool upd = r < sb[k];
-          sb[k] = upd ? r : sb[k];
-          path[k] = upd ? i : path[k];
-          const uint32_t key = (sb[k] << SP3_SH) | lo[k];  // (removed: lo = ~0)
+          // (a removed column never improves: r >= minVal >= its spc, and its
+          // t is older; its key is ~0 whatever sbp holds)
+          const uint32_t r = (uint32_t)Wp[k] + (uint32_t)cc[k] + bse;
+          sbp[k] = r < sbp[k] ? r : sbp[k];
+          const uint32_t key = (sbp[k] & SP3_KMASK) | lo[k];
           best = key < best ? key : best;
         }
         // the row of this lane's best column (byte best & 3 of r4c): formed in
-        // the DPP chain's wait states, one readlane of it below gives the next row
-        const uint32_t rsel = (r4c >> ((best & 3u) << 3)) & 0xFFu;
+        // the DPP chain's wait states, one readlane of it below gives the next
+        // row (the bit-field offset is (best << 3) mod 32)
+        const uint32_t rsel = __builtin_amdgcn_ubfe(r4c, best << 3, 8);
         const uint32_t g = wave_min_u32_dpp(best);
         if constexpr (TIMED) {
           asm volatile("" ::"s"(g));
           stamp(tB);
         }
         minVal = (int32_t)(g >> SP3_SH) - SP3_BIAS;
-        const int kw = (int)(g & 3u);
+        kw = (int)(g & 3u);
         const uint32_t pkey = (g >> 2) & 255u;
         const bool assigned = (g >> 10) & 1u;
         const int lw = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == g));
         const int pstar = assigned ? (int)pkey : 255 - (int)pkey;
         const int last = nrem - 1;
-        pglo = g & ((1u << SP3_SH) - 1u);
         kX = (uint32_t)(last ^ pstar) << 2;
-        mv = mover_v;
-        rem[pstar] = (uint8_t)mover_v;  // (every lane, same byte; a no-op when pstar == last)
+        wmask = 1ull << lw;
+        const int mv = __builtin_amdgcn_readfirstlane(mover_v);
+        mmask = 1ull << (mv >> 2);
+        kmv = mv & 3;
+        rem[pstar] = (uint32_t)mover_v;  // (every lane, same word; a no-op when pstar == last)
         --nrem;
         // (branch-free: both the winner's column and its row are formed; the
         // row is the next step's when assigned, the column is the sink if not)
@@ -3351,27 +3347,33 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         i = __builtin_amdgcn_readlane((int)rsel, lw);
         if (!assigned) break;
       }
-      // Dual update (scipy's, in V units, deferred to the Dijkstra's end): the columns that left
-      // `remaining` (lo = ~0; not the sink, whose update is 0) add
-      // minVal - spc to -v and to the dual of their row.
+      // Dual update (scipy's, in V units, deferred to the Dijkstra's end): the
+      // columns that left `remaining` (lo = ~0; not the sink, whose update is
+      // 0) add minVal - spc to -v and to the dual of their row.  Then each
+      // column's path row: the row of the step in sbp's low byte (rowq; an
+      // unreached column reads an unused in-bounds word).
       const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
+      int32_t prow[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
-        const int32_t dd = vk ? (int32_t)(mvb - sb[k]) : 0;
+        const int32_t dd = vk ? (int32_t)(mvb - (sbp[k] >> SP3_SH)) : 0;
         W[k] += dd;
+        Wp[k] = (int32_t)((uint32_t)W[k] << SP3_SH);
         accW |= (uint32_t)W[k] + LR.CW;
         const int ua = vk ? (int)((r4c >> (8 * k)) & 0xFFu) : 256 + lane;
         __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
       }
       if (lane == 0) u_l[cur] += minVal;
-      // augment along path[] from the sink back to cur (registers only)
+      // augment along the path from the sink back to cur (registers only)
       int j = sink;
       for (;;) {
         const int jl = j >> 2;
-        const int p0 = __builtin_amdgcn_readlane(path[0], jl), p1 = __builtin_amdgcn_readlane(path[1], jl);
-        const int p2 = __builtin_amdgcn_readlane(path[2], jl), p3 = __builtin_amdgcn_readlane(path[3], jl);
-        const int pi = (j & 2) ? ((j & 1) ? p3 : p2) : ((j & 1) ? p1 : p0);
+        const int p0 = __builtin_amdgcn_readlane(prow[0], jl), p1 = __builtin_amdgcn_readlane(prow[1], jl);
+        const int p2 = __builtin_amdgcn_readlane(prow[2], jl), p3 = __builtin_amdgcn_readlane(prow[3], jl);
+        const int pa = (j & 2) ? ((j & 1) ? p3 : p2) : ((j & 1) ? p1 : p0);
+        const int pi = (int)(((uint32_t)pa - ubase) >> 2);
         // row pi: its previous column t leaves, j becomes its column
         const int pl = pi >> 2, ps = 8 * (pi & 3);
         const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)c4r, pl);
