@@ -956,15 +956,18 @@ __device__ __forceinline__ bool sap_solve_mw_l32(const int n, const Loader &ld, 
     if (tid == 0) u32[cur] += minVal;
     __syncthreads();
     if (tid == 0) {  // augment along the path from the sink back to cur
-      int jj = sink;
-      for (;;) {
-        const int pi = S.path[jj];
+      // (at most n hops: a path that does not reach cur in n hops can only
+      // come from values outside the checked range; the block is redone)
+      int jj = sink, pi = -1;
+      for (int hop = 0; hop <= n; ++hop) {
+        pi = S.path[jj];
         S.r4c[jj] = (int16_t)pi;
         const int t = S.c4r[pi];
         S.c4r[pi] = (int16_t)jj;
         jj = t;
         if (pi == cur) break;
       }
+      big |= pi != cur;
     }
     __syncthreads();
   }
@@ -3162,12 +3165,19 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   u32x4 lo;            // (one VGPR tuple: a step's book-keeping writes lo[k] by an indexed move)
   uint32_t c4r = ~0u;  // column of row 4*lane + k in byte k
   uint32_t r4c = 0;    // row of column 4*lane + k in byte k (valid where assigned)
-  uint64_t AM[4];      // assigned columns (wave masks, SGPRs)
+  uint64_t AM[4];      // assigned columns (wave masks, SGPRs; a column, once assigned, stays so)
+  // the tie bits of column j = 4 lane + k at a Dijkstra's start (pos = n-1-j):
+  // (asg ? 256 | pos : 255 - pos) << 2 | k = P ^ (asg ? 0x400 : 0x3FC) with
+  // P = pos << 2 | k (255 - pos = pos ^ 255); a column j >= n (never
+  // assigned) has P = ~0x3FC, i.e. lo = ~0
+  uint32_t P[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     W[k] = 0;
     Wp[k] = 0;
     AM[k] = 0;
+    const int j = 4 * lane + k;
+    P[k] = j < n ? ((uint32_t)(n - 1 - j) << 2) | (uint32_t)k : ~0x3FCu;
   }
   // rem[p]: the column at position p of scipy's `remaining`; rowq[n - 1 - t]:
   // the LDS address of u_l[i] for the row i of step t (written by the step's
@@ -3199,11 +3209,8 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       asm volatile("" : "+v"(ln));
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int j = 4 * ln + k;
-        const uint32_t pos = (uint32_t)(n - 1 - j);
         const bool asg = __builtin_amdgcn_inverse_ballot_w64(AM[k]);
-        const uint32_t pk = asg ? ((1u << 8) | pos) : (255u - pos);
-        lo[k] = (j < n) ? ((pk << 2) | (uint32_t)k) : ~0u;
+        lo[k] = P[k] ^ (asg ? 0x400u : 0x3FCu);
         sbp[k] = ~0u;
       }
       {
@@ -3353,7 +3360,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       // column's path row: the row of the step in sbp's low byte (rowq; an
       // unreached column reads an unused in-bounds word).
       const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
-      int32_t prow[4];
+      i32x4 prow;  // (one VGPR tuple: the augmentation selects prow[j & 3] by an indexed move)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
@@ -3365,15 +3372,26 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
       }
-      if (lane == 0) u_l[cur] += minVal;
-      // augment along the path from the sink back to cur (registers only)
-      int j = sink;
-      for (;;) {
+      if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // the sink is the one column this Dijkstra assigns
+#pragma unroll
+      for (int k = 0; k < 4; ++k) AM[k] |= ((sink & 3) == k) ? 1ull << (sink >> 2) : 0ull;
+      // augment along the path from the sink back to cur (registers only; at
+      // most n hops -- a path that does not reach cur in n hops can only come
+      // from values outside the checked range, and the block is left to the
+      // fallback launch)
+      int j = sink, pi = -1;
+      for (int hop = 0; hop <= n; ++hop) {
         const int jl = j >> 2;
-        const int p0 = __builtin_amdgcn_readlane(prow[0], jl), p1 = __builtin_amdgcn_readlane(prow[1], jl);
-        const int p2 = __builtin_amdgcn_readlane(prow[2], jl), p3 = __builtin_amdgcn_readlane(prow[3], jl);
-        const int pa = (j & 2) ? ((j & 1) ? p3 : p2) : ((j & 1) ? p1 : p0);
-        const int pi = (int)(((uint32_t)pa - ubase) >> 2);
+        int pv;  // prow[j & 3] (one indexed move), then lane jl of it
+        asm volatile(
+            "s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\t"
+            "v_mov_b32 %0, %2\n\t"
+            "s_set_gpr_idx_off"
+            : "=v"(pv)
+            : "s"(j & 3), "v"(prow.x), "v"(prow));
+        const int pa = __builtin_amdgcn_readlane(pv, jl);
+        pi = (int)(((uint32_t)pa - ubase) >> 2);
         // row pi: its previous column t leaves, j becomes its column
         const int pl = pi >> 2, ps = 8 * (pi & 3);
         const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)c4r, pl);
@@ -3385,11 +3403,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const uint32_t rw = (uint32_t)__builtin_amdgcn_readlane((int)r4c, jl);
         const uint32_t nr4 = (rw & ~(0xFFu << js)) | ((uint32_t)pi << js);
         asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r4c) : "s"(nr4), "{m0}"(jl));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) AM[k] |= ((j & 3) == k) ? 1ull << jl : 0ull;
         j = t;
         if (pi == cur) break;
       }
+      bad |= pi != cur;
     }
   }
   stamp(tD);
