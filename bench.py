@@ -38,9 +38,11 @@ LDS_PEAK_TBS = 256 * 256 * 2.4e9 / 1e12
 # Algorithmic LDS bytes of the solve per Dijkstra step and per Dijkstra (all
 # lanes of the block's waves): santa_sp3_kernel per step =
 # 64 lanes x (4 scatter + 16 row read + 4 un-scatter + 4 u + 1 + 1 remaining),
-# per Dijkstra 64 x (4 remaining + 16 dual atomics); the 4-wave kernels per step = 256 threads
+# per Dijkstra 64 x (4 remaining + 16 dual atomics); santa_dt_kernel per step = 64 lanes x 4
+# tile bytes + 16 (u, mover, two one-lane stores), per Dijkstra 64 x (16 remaining + 16 dual
+# atomics + 4 path rows); the 4-wave kernels per step = 256 threads
 # x (1 tile byte + 4 u + 8 step word) + the fold, per Dijkstra 256 x 12.
-LDS_BYTES = {"santa_sp3_kernel": (64 * 30, 64 * 20),
+LDS_BYTES = {"santa_sp3_kernel": (64 * 30, 64 * 20), "santa_dt_kernel": (64 * 4 + 16, 64 * 36),
              "santa_block_kernel": (256 * 13, 256 * 12), "santa_vt_kernel": (256 * 12, 256 * 12)}
 CLOCK_HZ = 2.4e9               # MI355X max shader clock (MI355X_MICROARCH.md)
 KERNEL_SRC = os.path.join(ROOT, "mpi-hungarian-method_amd", "csrc", "santa_hip.hip")
@@ -500,7 +502,8 @@ def main():
         bmax = int(st[0].argmax())
         rows0 = ctx.sample_blocks(mode, n, nb, args.seed, 0)
         one = rows0[(b0 + bmax) * n:(b0 + bmax + 1) * n].contiguous()
-        force = {0: _lib.SH_FLAG_SP_TILE, 7: _lib.SH_FLAG_SP_TILE, 1: _lib.SH_FLAG_LDS_TILE}.get(design, 0)
+        force = {0: _lib.SH_FLAG_SP_TILE, 7: _lib.SH_FLAG_SP_TILE, 1: _lib.SH_FLAG_LDS_TILE,
+                 8: _lib.SH_FLAG_DT_TILE}.get(design, 0)
         lone = []
         for _ in range(3):
             tt = ctx.upload_types(sd.types)

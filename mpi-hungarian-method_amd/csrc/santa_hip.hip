@@ -1188,24 +1188,16 @@ __host__ __device__ __forceinline__ SantaLds santa_lds_layout(int n, int mode, i
   return L;
 }
 
-template <int K, int MODE, bool TIMED = false>
-__global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
-  static_assert(K == 1, "one column per thread (n <= 256)");
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int b = blockIdx.x;
+// The 4-wave dense tile build of the LDS-tile kernels: the block's rows
+// (range-checked), the column gift types (range-checked: they index LDS
+// tables), the type -> column chains, then the rank code of every wish into
+// tile8[i * RS + j] (twins: code pairs).  All SANTA_WG threads call it; false
+// (after setting the error flag) when the block's rows or types are bad.
+template <int MODE>
+__device__ __forceinline__ bool lds_tile_build(const SantaArgs &a, const int b, const int n, const int RS,
+                                               uint8_t *tile8, int32_t *rows_l, int16_t *ctype, int32_t *head,
+                                               int16_t *nxt) {
   const int tid = threadIdx.x;
-  const int n = a.n;
-  const SantaLds L = santa_lds_layout(n, MODE, a.ng);
-  const int RS = L.RS;
-  uint8_t *tile8 = smem + L.tile;
-  int32_t *rows_l = (int32_t *)(smem + L.rows);
-  int16_t *ctype = (int16_t *)(smem + L.ctype);
-  int32_t *head = (int32_t *)(smem + L.head);
-  int16_t *nxt = (int16_t *)(smem + L.nxt);
-  int64_t *part = (int64_t *)(smem + L.part);
-  SolveLds S{(int64_t *)(smem + L.u), (int16_t *)(smem + L.c4r), (int16_t *)(smem + L.r4c),
-             (int16_t *)(smem + L.path), (uint64_t *)(smem + L.red)};
-
   // -- rows of this block, range check -----------------------------------
   int bad = 0;
   for (int j = tid; j < n; j += SANTA_WG) {
@@ -1215,7 +1207,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   }
   if (__syncthreads_or(bad)) {
     if (tid == 0) atomicOr(a.err, SH_ERRF_ROWS);
-    return;
+    return false;
   }
   for (int t = tid; t < a.ng; t += SANTA_WG) head[t] = -1;
   {
@@ -1232,7 +1224,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   }
   if (__syncthreads_or(badt)) {
     if (tid == 0) atomicOr(a.err, SH_ERRF_TYPE);
-    return;
+    return false;
   }
   // -- type -> column chains ------------------------------------------------
   for (int j = tid; j < n; j += SANTA_WG) nxt[j] = (int16_t)atomicExch(&head[ctype[j]], j);
@@ -1297,6 +1289,28 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
       }
     }
   }
+  return true;
+}
+
+template <int K, int MODE, bool TIMED = false>
+__global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
+  static_assert(K == 1, "one column per thread (n <= 256)");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int n = a.n;
+  const SantaLds L = santa_lds_layout(n, MODE, a.ng);
+  const int RS = L.RS;
+  uint8_t *tile8 = smem + L.tile;
+  int32_t *rows_l = (int32_t *)(smem + L.rows);
+  int16_t *ctype = (int16_t *)(smem + L.ctype);
+  int32_t *head = (int32_t *)(smem + L.head);
+  int16_t *nxt = (int16_t *)(smem + L.nxt);
+  int64_t *part = (int64_t *)(smem + L.part);
+  SolveLds S{(int64_t *)(smem + L.u), (int16_t *)(smem + L.c4r), (int16_t *)(smem + L.r4c),
+             (int16_t *)(smem + L.path), (uint64_t *)(smem + L.red)};
+
+  if (!lds_tile_build<MODE>(a, b, n, RS, tile8, rows_l, ctype, head, nxt)) return;
   for (int i = tid; i < n; i += SANTA_WG) {
     S.u[i] = 0;
     S.c4r[i] = -1;
@@ -3076,8 +3090,13 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
             const uint32_t hz = h[z];
             const uint32_t A = (uint32_t)(nw - r) << 9;
             const int cg = (int)(hz >> 24);
-            srow[(cg >= 1 && x < lim) ? x : 32] = (uint16_t)((hz & 0xFFu) | A);
-            srow[(cg >= 2 && x + 1 < lim) ? x + 1 : 32] = (uint16_t)(((hz >> 8) & 0xFFu) | A);
+            // the type's first two columns at x, x + 1 whatever cg is: a
+            // slot past the row's hits so far is rewritten by the next hit or
+            // lies past the row's count (the transpose masks it by rcnt);
+            // positions from 32 on fall on the dump slot 32, and an
+            // overflowing row's slot 31 is its marker (set by the transpose)
+            srow[min(x, 32)] = (uint16_t)((hz & 0xFFu) | A);
+            srow[min(x, 31) + 1] = (uint16_t)(((hz >> 8) & 0xFFu) | A);
             if (__any(cg >= 3)) {
               if (cg == 3) {
                 srow[x + 2 < lim ? x + 2 : 32] = (uint16_t)(((hz >> 16) & 0xFFu) | A);
@@ -3217,6 +3236,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const int p0 = n - 1 - 4 * ln;
         *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
       }
+      if (lane == 0) rowq[n - 1] = ubase + 4u * (uint32_t)cur;  // (step 0's row)
       int nrem = n;
       int32_t minVal = 0;
       int i = cur;
@@ -3228,6 +3248,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       uint64_t wmask = 0, mmask = 0;
       int kw = 0, kmv = 0;
       uint32_t kX = 0;
+      uint32_t rpa = 0;  // the previous step's rem[pstar] address
+      // the mover: the previous step's, stored by the group, then replaced by
+      // this step's read (one register: the store reads it at issue)
+      int mover_v = 0;
       bool first = true;
       for (;;) {
         ++steps;
@@ -3248,31 +3272,36 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           stamp(tA1);
         }
         int32_t uraw;
-        int mover_v;  // the column at the last position of `remaining`
         int2 c01, c23;
         // The step's LDS traffic as one issue group for every row (a row with
         // more than 32 hits has the marker, whose slot is a dump slot, in its
-        // entry 31; such a row re-reads its columns below): the dual and the
-        // mover, the scatter, the row reads, the un-scatter, the step's row
-        // (rowq[nrem - 1] = the dual's address) -- no wait in between; then
-        // the previous step's book-keeping in their shadow, one lane and one
-        // register each (exec = that lane, the slot by GPR indexing on the lo
-        // tuple, %17 = its first register), one wait at the end.  Operands stay
-        // live through that wait.
+        // entry 31; such a row re-reads its columns below), no wait in between:
+        // by one lane (exec = the previous step's winner lane; none on a
+        // Dijkstra's first step) the previous step's rem[pstar] = mover and
+        // this step's row (rowq[nrem - 1] = the dual's address; step 0's is
+        // written at the set-up) -- a store of one word by all 64 lanes costs
+        // the LDS a 64-way bank conflict; then the dual and the mover, the
+        // scatter, the row reads, the un-scatter; then the previous step's
+        // book-keeping in their shadow, one lane and one register each (exec =
+        // that lane, the slot by GPR indexing on the lo tuple, %17 = its first
+        // register); one wait at the end.  Operands stay live through that wait.
         const uint32_t ua = ubase + 4u * (uint32_t)i;
         const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
         const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
         const int32_t miss = SP3_MISS;
         uint64_t sv;
         asm volatile(
+            "s_mov_b64 %4, exec\n\t"
+            "s_mov_b64 exec, %12\n\t"
+            "ds_write_b32 %18, %1\n\t"
+            "ds_write_b32 %7, %6 offset:1024\n\t"
+            "s_mov_b64 exec, %4\n\t"
             "ds_read_b32 %0, %6\n\t"
             "ds_read_b32 %1, %7\n\t"
             "ds_write_b32 %8, %9\n\t"
             "ds_read2_b32 %2, %10 offset1:1\n\t"
             "ds_read2_b32 %3, %10 offset0:128 offset1:129\n\t"
             "ds_write_b32 %8, %11\n\t"
-            "ds_write_b32 %7, %6 offset:1024\n\t"
-            "s_mov_b64 %4, exec\n\t"
             "s_mov_b64 exec, %12\n\t"
             "s_set_gpr_idx_on %13, gpr_idx(DST)\n\t"
             "v_mov_b32 %17, -1\n\t"
@@ -3283,9 +3312,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
             "s_set_gpr_idx_off\n\t"
             "s_mov_b64 exec, %4\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "=&s"(sv), "+v"(lo)
+            : "=&v"(uraw), "+v"(mover_v), "=&v"(c01), "=&v"(c23), "=&s"(sv), "+v"(lo)
             : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(miss), "s"(wmask), "s"(kw), "s"(mmask),
-              "s"(kmv), "s"(kX), "v"(lo.x)
+              "s"(kmv), "s"(kX), "v"(lo.x), "v"(rpa)
             : "memory");
         // (a row with more than 32 hits: the tile's entries and the overflow
         // list scattered again, the four columns re-read; the other half's
@@ -3346,7 +3375,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
         mmask = 1ull << (mv >> 2);
         kmv = mv & 3;
-        rem[pstar] = (uint32_t)mover_v;  // (every lane, same word; a no-op when pstar == last)
+        rpa = lds_addr(rem) + 4u * (uint32_t)pstar;  // (stored by the next step's group; a no-op when pstar == last)
         --nrem;
         // (branch-free: both the winner's column and its row are formed; the
         // row is the next step's when assigned, the column is the sink if not)
@@ -3483,6 +3512,565 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
       atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// santa_dt_kernel (round 4): few-block singles launches -- one GPU's shard of
+// a round at 4 or 8 GPUs, at most two blocks per CU.  Four waves build the
+// block's dense uint8 rank-code tile in LDS (lds_tile_build, as the 4-wave
+// LDS-tile kernel); then waves 1-3 leave and wave 0 alone runs
+// santa_sp3_kernel's one-wave solve (key units, one DPP argmin per step, no
+// cross-wave exchange and no barrier) with the row read straight from the
+// tile: one ds_read_b32 per lane gives the codes of its columns 4 lane ..
+// 4 lane + 3 (no scatter, no hit list, no overflow).  The 4-wave LDS-tile
+// step pays ~450 cycles for its exchange (ds_min_u64 fold, barrier, read);
+// the sparse step pays for expanding a hit list into a row buffer.
+// A block that leaves the lattice range goes to the fallback launch, as in
+// santa_sp3_kernel.  LDS: the 64 KB tile + ~10 KB, two blocks per CU.
+// ---------------------------------------------------------------------------
+constexpr int DT_RS = 256;  // tile row stride (bytes): a lane's four columns are one dword
+struct DtLds {
+  size_t tile, u, rows, ctype, rem, head, nxt, total;
+};
+__host__ __device__ __forceinline__ DtLds dt_lds_layout(int n, int ng) {
+  DtLds L;
+  size_t off = 0;
+  L.tile = off;  off += (size_t)n * DT_RS;
+  L.u = off;     off += (256 + 64) * 4;  // row duals (int32) + a dump slot per lane
+  L.rows = off;  off += r16((size_t)n * 4);
+  L.ctype = off; off += r16((size_t)n * 2);
+  L.rem = off;   off += 512 * 4;         // `remaining`, then the rows by step (santa_sp3_kernel)
+  L.head = off;  off += r16((size_t)ng * 4);
+  L.nxt = off;   off += r16((size_t)n * 2);
+  L.total = off;
+  return L;
+}
+
+__global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int n = a.n;
+  const DtLds L = dt_lds_layout(n, a.ng);
+  uint8_t *tile8 = smem + L.tile;
+  int32_t *u_l = (int32_t *)(smem + L.u);
+  int32_t *rows_l = (int32_t *)(smem + L.rows);
+  int16_t *ctype = (int16_t *)(smem + L.ctype);
+  uint32_t *rem = (uint32_t *)(smem + L.rem);
+  if (!lds_tile_build<0>(a, b, n, DT_RS, tile8, rows_l, ctype, (int32_t *)(smem + L.head),
+                         (int16_t *)(smem + L.nxt)))
+    return;
+  __syncthreads();
+  if (tid >= WAVE) return;  // (wave 0 solves; no barrier from here on)
+  const int lane = tid;
+  const int nw1 = a.n_wish + 1;
+  const int64_t E = a.E;
+  for (int r = lane; r < 256 + 64; r += WAVE) u_l[r] = 0;
+  const int Mm = (int)min((int64_t)199, (int64_t)(0xFFFFFFFFll / E) / 2);
+  const LatticeRange LR(Mm);
+  __builtin_amdgcn_s_setprio(3);
+
+  // state per column 4 lane + k as in santa_sp3_kernel (key units, see there);
+  // a tile code c (rank + 1, 0 = miss) enters as c << 20 with -nw1 << 20
+  // folded into the step's scalar: a wish (c - nw1) * 512 and a miss 1 in
+  // V units, i.e. a miss enters as MK = 2^11 + (nw1 << 20)
+  const uint32_t MK = (uint32_t)SP3_MISS + ((uint32_t)nw1 << 20);
+  uint32_t sbp[4];
+  int32_t W[4], Wp[4];
+  u32x4 lo;
+  uint32_t c4r = ~0u, r4c = 0;
+  uint64_t AM[4];
+  uint32_t P[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    W[k] = 0;
+    Wp[k] = 0;
+    AM[k] = 0;
+    const int j = 4 * lane + k;
+    P[k] = j < n ? ((uint32_t)(n - 1 - j) << 2) | (uint32_t)k : ~0x3FCu;
+  }
+  uint32_t *rowq = rem + 256;
+  const uint32_t ubase = lds_addr(u_l);
+  const uint32_t tbase = lds_addr(tile8) + 4u * (uint32_t)lane;
+  int steps = 0;
+  bool bad = (a.flags & (SH_FLAG_TEST_RANGE | SH_FLAG_EXACT_ARGMIN)) != 0 || !LR.ok;
+  uint32_t accU = 0, accW = 0;
+  if (a.flags & SH_FLAG_BUILD_ONLY) {
+    c4r = (uint32_t)(4 * lane) * 0x01010101u + 0x03020100u;
+  } else {
+    for (int cur = 0; cur < n; ++cur) {
+      if (cur == n - SP3_PRIO_A) __builtin_amdgcn_s_setprio(2);
+      if (cur == n - SP3_PRIO_B) __builtin_amdgcn_s_setprio(1);
+      if (cur == n - SP3_PRIO_C) __builtin_amdgcn_s_setprio(0);
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool asg = __builtin_amdgcn_inverse_ballot_w64(AM[k]);
+        lo[k] = P[k] ^ (asg ? 0x400u : 0x3FCu);
+        sbp[k] = ~0u;
+      }
+      {
+        const int p0 = n - 1 - 4 * ln;
+        *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
+      }
+      if (lane == 0) rowq[n - 1] = ubase + 4u * (uint32_t)cur;  // (step 0's row)
+      int nrem = n;
+      int32_t minVal = 0;
+      int i = cur;
+      int sink;
+      uint64_t wmask = 0, mmask = 0;
+      int kw = 0, kmv = 0;
+      uint32_t kX = 0;
+      uint32_t rpa = 0;
+      int mover_v = 0;
+      for (;;) {
+        ++steps;
+        int32_t uraw;
+        uint32_t w4;  // the codes of this lane's four columns in row i
+        const uint32_t ua = ubase + 4u * (uint32_t)i;
+        const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
+        const uint32_t ta = tbase + (uint32_t)i * DT_RS;
+        uint64_t sv;
+        // the step's LDS group (santa_sp3_kernel's, with the tile row read
+        // in place of the scatter / row reads / un-scatter), the previous
+        // step's book-keeping in its shadow, one wait
+        asm volatile(
+            "s_mov_b64 %3, exec\n\t"
+            "s_mov_b64 exec, %9\n\t"
+            "ds_write_b32 %14, %1\n\t"
+            "ds_write_b32 %6, %5 offset:1024\n\t"
+            "s_mov_b64 exec, %3\n\t"
+            "ds_read_b32 %2, %7\n\t"
+            "ds_read_b32 %0, %5\n\t"
+            "ds_read_b32 %1, %6\n\t"
+            "s_mov_b64 exec, %9\n\t"
+            "s_set_gpr_idx_on %10, gpr_idx(DST)\n\t"
+            "v_mov_b32 %8, -1\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %11\n\t"
+            "s_set_gpr_idx_on %12, gpr_idx(SRC1,DST)\n\t"
+            "v_xor_b32 %8, %13, %8\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %3\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(uraw), "+v"(mover_v), "=&v"(w4), "=&s"(sv), "+v"(lo)
+            : "v"(ua), "v"(ra), "v"(ta), "v"(lo.x), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv), "s"(kX), "v"(rpa)
+            : "memory");
+        const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
+        accU |= (uint32_t)ui + LR.CU;
+        uint32_t bse = ((uint32_t)(SP3_BIAS - ui) << SP3_SH) - ((uint32_t)nw1 << 20) + (uint32_t)(n - nrem);
+        asm volatile("" : "+s"(bse));
+        uint32_t best = ~0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t code = (w4 >> (8 * k)) & 0xFFu;
+          const uint32_t c = code ? code << 20 : MK;
+          const uint32_t r = (uint32_t)Wp[k] + c + bse;
+          sbp[k] = r < sbp[k] ? r : sbp[k];
+          const uint32_t key = (sbp[k] & SP3_KMASK) | lo[k];
+          best = key < best ? key : best;
+        }
+        const uint32_t rsel = __builtin_amdgcn_ubfe(r4c, best << 3, 8);
+        const uint32_t g = wave_min_u32_dpp(best);
+        minVal = (int32_t)(g >> SP3_SH) - SP3_BIAS;
+        kw = (int)(g & 3u);
+        const uint32_t pkey = (g >> 2) & 255u;
+        const bool assigned = (g >> 10) & 1u;
+        const int lw = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == g));
+        const int pstar = assigned ? (int)pkey : 255 - (int)pkey;
+        const int last = nrem - 1;
+        kX = (uint32_t)(last ^ pstar) << 2;
+        wmask = 1ull << lw;
+        const int mv = __builtin_amdgcn_readfirstlane(mover_v);
+        mmask = 1ull << (mv >> 2);
+        kmv = mv & 3;
+        rpa = lds_addr(rem) + 4u * (uint32_t)pstar;
+        --nrem;
+        sink = 4 * lw + kw;
+        i = __builtin_amdgcn_readlane((int)rsel, lw);
+        if (!assigned) break;
+      }
+      // dual update, path rows, augmentation: santa_sp3_kernel's
+      const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
+      i32x4 prow;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
+        const int32_t dd = vk ? (int32_t)(mvb - (sbp[k] >> SP3_SH)) : 0;
+        W[k] += dd;
+        Wp[k] = (int32_t)((uint32_t)W[k] << SP3_SH);
+        accW |= (uint32_t)W[k] + LR.CW;
+        const int ua = vk ? (int)((r4c >> (8 * k)) & 0xFFu) : 256 + lane;
+        __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
+      }
+      if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) AM[k] |= ((sink & 3) == k) ? 1ull << (sink >> 2) : 0ull;
+      int j = sink, pi = -1;
+      for (int hop = 0; hop <= n; ++hop) {
+        const int jl = j >> 2;
+        int pv;
+        asm volatile(
+            "s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\t"
+            "v_mov_b32 %0, %2\n\t"
+            "s_set_gpr_idx_off"
+            : "=v"(pv)
+            : "s"(j & 3), "v"(prow.x), "v"(prow));
+        const int pa = __builtin_amdgcn_readlane(pv, jl);
+        pi = (int)(((uint32_t)pa - ubase) >> 2);
+        const int pl = pi >> 2, ps = 8 * (pi & 3);
+        const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)c4r, pl);
+        const int t = (int)((cw >> ps) & 0xFFu);
+        const uint32_t nw4 = (cw & ~(0xFFu << ps)) | ((uint32_t)j << ps);
+        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(c4r) : "s"(nw4), "{m0}"(pl));
+        const int js = 8 * (j & 3);
+        const uint32_t rw = (uint32_t)__builtin_amdgcn_readlane((int)r4c, jl);
+        const uint32_t nr4 = (rw & ~(0xFFu << js)) | ((uint32_t)pi << js);
+        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r4c) : "s"(nr4), "{m0}"(jl));
+        j = t;
+        if (pi == cur) break;
+      }
+      bad |= pi != cur;
+    }
+  }
+  // the lattice range (see santa_sp3_kernel): leave the block to the fallback
+  // launch (the outputs come from the tile, so the final duals need no check)
+  if (__builtin_expect(__any(bad || ((accU & LR.MU) | (accW & LR.MW)) != 0), 0)) {
+    if (lane == 0) {
+      const int p = atomicAdd(a.ovf_cnt, 1);
+      a.ovf_list[p] = b;
+    }
+    return;
+  }
+  int64_t cost = 0, dch = 0, dgh = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int i = 4 * lane + k;
+    if (i < n) {
+      const int col = (int)((c4r >> (8 * k)) & 0xFFu);
+      const uint32_t cn = tile8[(size_t)i * DT_RS + col];
+      const uint32_t co = tile8[(size_t)i * DT_RS + i];
+      const int told = ctype[i], tnew = ctype[col];
+      const int chd = rows_l[i];
+      cost += single_cost(cn, nw1, E);
+      dch += child_happy(cn, nw1) - child_happy(co, nw1);
+      if (a.delta) dgh += gift_happy(a, chd, tnew) - gift_happy(a, chd, told);
+      if (a.col) a.col[(size_t)b * n + i] = col;
+      if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[chd] = (int16_t)tnew;  // this block owns chd
+    }
+  }
+  cost = wave_sum_i64(cost);
+  dch = wave_sum_i64(dch);
+  dgh = wave_sum_i64(dgh);
+  if (lane == 0) {
+    if (a.cost) a.cost[b] = cost;
+    if (a.steps) a.steps[b] = steps;
+    if (a.delta) {
+      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
+      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// santa_dtw_kernel (round 4): twins blocks (n <= 256 pairs; a round has 78,
+// one per CU) with santa_dt_kernel's plan in 64-bit scaled units.  Four waves
+// build the uint16 code-pair tile (lds_tile_build<1> + the twin_entry
+// re-code) as santa_block_kernel<1, 1>; then wave 0 alone solves with four
+// columns per lane, keys of sap_solve_mw_sc (every value x 2^SC_SH, so
+// sbp = spc + SC_BIAS has 17 zero low bits: the Dijkstra step t of the
+// column's last improvement sits in the low byte, as in santa_sp3_kernel)
+// and a two-word DPP argmin (high words, then the low words of the lanes at
+// the minimum), no cross-wave exchange.  A block outside the scaled range
+// (or under SH_FLAG_TEST_RANGE / SH_FLAG_EXACT_ARGMIN) is re-solved by all
+// four waves with the windowed-key solver, as santa_block_kernel does.
+// ---------------------------------------------------------------------------
+// the 4-wave twins layout + `remaining` / rows by step (512 x 4 B), the
+// one-wave solve's row duals (320 x 8 B) and two flag words
+__host__ __device__ __forceinline__ size_t dtw_lds_bytes(int n, int ng) {
+  return santa_lds_layout(n, 1, ng).total + 512 * 4 + 320 * 8 + 16;
+}
+
+__global__ __launch_bounds__(SANTA_WG) void santa_dtw_kernel(SantaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int n = a.n;
+  const SantaLds L = santa_lds_layout(n, 1, a.ng);
+  const int RS = L.RS;
+  uint8_t *tile8 = smem + L.tile;
+  int32_t *rows_l = (int32_t *)(smem + L.rows);
+  int16_t *ctype = (int16_t *)(smem + L.ctype);
+  int64_t *part = (int64_t *)(smem + L.part);
+  SolveLds S{(int64_t *)(smem + L.u), (int16_t *)(smem + L.c4r), (int16_t *)(smem + L.r4c),
+             (int16_t *)(smem + L.path), (uint64_t *)(smem + L.red)};
+  uint32_t *rem = (uint32_t *)(smem + L.total);               // [512]: remaining, rows by step
+  int64_t *u_l = (int64_t *)(smem + L.total + 512 * 4);        // [256 + 64]: row duals + dumps
+  int32_t *flag = (int32_t *)(smem + L.total + 512 * 4 + 320 * 8);  // [2]: redo, steps
+  if (!lds_tile_build<1>(a, b, n, RS, tile8, rows_l, ctype, (int32_t *)(smem + L.head), (int16_t *)(smem + L.nxt)))
+    return;
+  const int nw1 = a.n_wish + 1;
+  const uint32_t E32 = (uint32_t)a.E;
+  __syncthreads();  // (the build's last code pairs)
+  {
+    uint4 *t4 = (uint4 *)tile8;
+    const int cnt4 = n * RS / 8;
+    auto rc2 = [&](uint32_t w) -> uint32_t {
+      return twin_entry(w & 0xFFFFu, nw1, a.E) | (twin_entry(w >> 16, nw1, a.E) << 16);
+    };
+    for (int q = tid; q < cnt4; q += SANTA_WG) {
+      const uint4 v = t4[q];
+      t4[q] = make_uint4(rc2(v.x), rc2(v.y), rc2(v.z), rc2(v.w));
+    }
+  }
+  for (int i = tid; i < n; i += SANTA_WG) {
+    S.u[i] = 0;
+    S.c4r[i] = -1;
+    S.r4c[i] = -1;
+  }
+  for (int r = tid; r < 256 + 64; r += SANTA_WG) u_l[r] = 0;
+  const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
+  const bool build_only = (a.flags & SH_FLAG_BUILD_ONLY) != 0;
+  bool redo = exact || (a.flags & SH_FLAG_TEST_RANGE) != 0;
+  __syncthreads();
+  if (tid < WAVE && !redo && !build_only) {
+    const int lane = tid;
+    uint64_t sbp[4];
+    int64_t W[4];
+    u32x4 lo, hm;  // tie bits; hm: ~0 once the column left `remaining` (the key's high word)
+    uint32_t c4r = ~0u, r4c = 0;
+    uint64_t AM[4];
+    uint32_t P[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      W[k] = 0;
+      AM[k] = 0;
+      const int j = 4 * lane + k;
+      P[k] = j < n ? ((uint32_t)(n - 1 - j) << 2) | (uint32_t)k : ~0x3FCu;
+    }
+    uint32_t *rowq = rem + 256;
+    const uint32_t ubase = lds_addr(u_l);
+    const uint32_t tbase = lds_addr(tile8) + 8u * (uint32_t)lane;
+    int steps = 0;
+    bool big = false;
+    __builtin_amdgcn_s_setprio(3);
+    for (int cur = 0; cur < n; ++cur) {
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool asg = __builtin_amdgcn_inverse_ballot_w64(AM[k]);
+        lo[k] = P[k] ^ (asg ? 0x400u : 0x3FCu);
+        hm[k] = (4 * ln + k < n) ? 0u : ~0u;
+        sbp[k] = ~0ull;
+      }
+      {
+        const int p0 = n - 1 - 4 * ln;
+        *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
+      }
+      if (lane == 0) rowq[n - 1] = ubase + 8u * (uint32_t)cur;  // (step 0's row)
+      int nrem = n;
+      int64_t minVal = 0;
+      int i = cur;
+      int sink;
+      uint64_t wmask = 0, mmask = 0;
+      int kw = 0, kmv = 0;
+      uint32_t kX = 0;
+      uint32_t rpa = 0;
+      int mover_v = 0;
+      for (;;) {
+        ++steps;
+        uint64_t uraw;
+        uint2 e4;  // the entries of this lane's four columns in row i
+        const uint32_t ua = ubase + 8u * (uint32_t)i;
+        const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
+        const uint32_t ta = tbase + (uint32_t)i * (2u * (uint32_t)RS);
+        uint64_t sv;
+        asm volatile(
+            "s_mov_b64 %3, exec\n\t"
+            "s_mov_b64 exec, %11\n\t"
+            "ds_write_b32 %16, %1\n\t"
+            "ds_write_b32 %7, %6 offset:1024\n\t"
+            "s_mov_b64 exec, %3\n\t"
+            "ds_read_b64 %2, %8\n\t"
+            "ds_read_b64 %0, %6\n\t"
+            "ds_read_b32 %1, %7\n\t"
+            "s_mov_b64 exec, %11\n\t"
+            "s_set_gpr_idx_on %12, gpr_idx(DST)\n\t"
+            "v_mov_b32 %9, -1\n\t"
+            "v_mov_b32 %10, -1\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %13\n\t"
+            "s_set_gpr_idx_on %14, gpr_idx(SRC1,DST)\n\t"
+            "v_xor_b32 %9, %15, %9\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %3\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(uraw), "+v"(mover_v), "=&v"(e4), "=&s"(sv), "+v"(lo), "+v"(hm)
+            : "v"(ua), "v"(ra), "v"(ta), "v"(lo.x), "v"(hm.x), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv),
+              "s"(kX), "v"(rpa)
+            : "memory");
+        const int64_t ui = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uraw >> 32)) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)uraw));
+        uint64_t bse = SC_BIAS - (uint64_t)(ui - minVal) + (uint64_t)(n - nrem);
+        asm volatile("" : "+s"(bse));
+        const uint32_t ent[4] = {e4.x & 0xFFFFu, e4.x >> 16, e4.y & 0xFFFFu, e4.y >> 16};
+        uint32_t bh = ~0u, bl = ~0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint64_t r = (uint64_t)W[k] + (uint64_t)twin_entry_cost<SC_SH>(ent[k], E32) + bse;
+          sbp[k] = r < sbp[k] ? r : sbp[k];
+          const uint32_t kh = (uint32_t)(sbp[k] >> 32) | hm[k];
+          const uint32_t kl = ((uint32_t)sbp[k] & ~SC_TIE_MASK) | lo[k];
+          const bool lt = kh < bh || (kh == bh && kl < bl);
+          bh = lt ? kh : bh;
+          bl = lt ? kl : bl;
+        }
+        const uint32_t rsel = __builtin_amdgcn_ubfe(r4c, bl << 3, 8);
+        const uint32_t gh = wave_min_u32_dpp(bh);
+        const uint32_t gl = wave_min_u32_dpp(bh == gh ? bl : ~0u);
+        minVal = (int64_t)((((uint64_t)gh << 32) | (gl & ~SC_TIE_MASK)) - SC_BIAS);
+        kw = (int)(gl & 3u);
+        const uint32_t pkey = (gl >> 2) & 255u;
+        const bool assigned = (gl >> 10) & 1u;
+        const int lw = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(bh == gh && bl == gl));
+        const int pstar = assigned ? (int)pkey : 255 - (int)pkey;
+        const int last = nrem - 1;
+        kX = (uint32_t)(last ^ pstar) << 2;
+        wmask = 1ull << lw;
+        const int mv = __builtin_amdgcn_readfirstlane(mover_v);
+        mmask = 1ull << (mv >> 2);
+        kmv = mv & 3;
+        rpa = lds_addr(rem) + 4u * (uint32_t)pstar;
+        --nrem;
+        sink = 4 * lw + kw;
+        i = __builtin_amdgcn_readlane((int)rsel, lw);
+        if (!assigned) break;
+      }
+      big |= (uint64_t)(minVal + SC_LIM) >= 2 * (uint64_t)SC_LIM;
+      i32x4 prow;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
+        const int64_t dd = vk ? minVal - (int64_t)((sbp[k] & ~(uint64_t)SC_TIE_MASK) - SC_BIAS) : 0;
+        W[k] += dd;
+        const int ua = vk ? (int)((r4c >> (8 * k)) & 0xFFu) : 256 + lane;
+        __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
+      }
+      if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) AM[k] |= ((sink & 3) == k) ? 1ull << (sink >> 2) : 0ull;
+      int j = sink, pi = -1;
+      for (int hop = 0; hop <= n; ++hop) {
+        const int jl = j >> 2;
+        int pv;
+        asm volatile(
+            "s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\t"
+            "v_mov_b32 %0, %2\n\t"
+            "s_set_gpr_idx_off"
+            : "=v"(pv)
+            : "s"(j & 3), "v"(prow.x), "v"(prow));
+        const int pa = __builtin_amdgcn_readlane(pv, jl);
+        pi = (int)(((uint32_t)pa - ubase) >> 3);
+        const int pl = pi >> 2, ps = 8 * (pi & 3);
+        const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)c4r, pl);
+        const int t = (int)((cw >> ps) & 0xFFu);
+        const uint32_t nw4 = (cw & ~(0xFFu << ps)) | ((uint32_t)j << ps);
+        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(c4r) : "s"(nw4), "{m0}"(pl));
+        const int js = 8 * (j & 3);
+        const uint32_t rw = (uint32_t)__builtin_amdgcn_readlane((int)r4c, jl);
+        const uint32_t nr4 = (rw & ~(0xFFu << js)) | ((uint32_t)pi << js);
+        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r4c) : "s"(nr4), "{m0}"(jl));
+        j = t;
+        if (pi == cur) break;
+      }
+      big |= pi != cur;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      big |= (uint64_t)(W[k] + SC_LIM) >= 2 * (uint64_t)SC_LIM;
+      if (4 * lane + k < n) big |= (uint64_t)(u_l[4 * lane + k] + SC_LIM) >= 2 * (uint64_t)SC_LIM;
+    }
+    const bool any_big = __any(big);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (4 * lane + k < n) S.c4r[4 * lane + k] = (int16_t)((c4r >> (8 * k)) & 0xFFu);
+    if (lane == 0) {
+      flag[0] = any_big ? 1 : 0;
+      flag[1] = steps;
+    }
+  }
+  __syncthreads();
+  int64_t steps = 0;
+  int fallbacks = 0;
+  if (!redo && !build_only) {
+    redo = flag[0] != 0;
+    steps = flag[1];
+  }
+  if (build_only) {
+    for (int i = tid; i < n; i += SANTA_WG) S.c4r[i] = (int16_t)i;
+    __syncthreads();
+  } else if (redo) {  // (block-uniform) the windowed-key solver, all four waves
+    for (int i = tid; i < n; i += SANTA_WG) {
+      S.u[i] = 0;
+      S.c4r[i] = -1;
+      S.r4c[i] = -1;
+    }
+    __syncthreads();
+    const TileU16Loader<SANTA_NW, 1> ld{(const uint16_t *)tile8, E32, RS};
+    sap_solve_mw<SANTA_NW, 1>(n, ld, S, steps, fallbacks, exact);
+  }
+  // -- outputs (santa_block_kernel<1, 1>'s) --------------------------------------
+  int64_t cost = 0, dch = 0, dgh = 0;
+  for (int i = tid; i < n; i += SANTA_WG) {
+    const int col = S.c4r[i];
+    if (a.col) a.col[(size_t)b * n + i] = col;
+    const int told = ctype[i], tnew = ctype[col];
+    const int child = rows_l[i];
+    const uint16_t *t16 = (const uint16_t *)tile8;
+    const uint32_t cn = t16[(size_t)i * RS + col];
+    const uint32_t co = t16[(size_t)i * RS + i];
+    cost += twin_entry_cost<0>(cn, E32);
+    dch += twin_entry_happy(cn) - twin_entry_happy(co);
+    if (a.delta)
+      dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) - gift_happy(a, child, told) -
+             gift_happy(a, child + 1, told);
+  }
+  cost = wave_sum_i64(cost);
+  dch = wave_sum_i64(dch);
+  dgh = wave_sum_i64(dgh);
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) {
+    part[3 * w + 0] = cost;
+    part[3 * w + 1] = dch;
+    part[3 * w + 2] = dgh;
+  }
+  for (int i = tid; i < n; i += SANTA_WG) {
+    const int16_t tnew = ctype[S.c4r[i]];
+    if (!(a.flags & SH_FLAG_NO_APPLY)) {
+      a.types[rows_l[i]] = tnew;
+      a.types[rows_l[i] + 1] = tnew;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int64_t tc = 0, td0 = 0, td1 = 0;
+    for (int q = 0; q < SANTA_NW; ++q) {
+      tc += part[3 * q];
+      td0 += part[3 * q + 1];
+      td1 += part[3 * q + 2];
+    }
+    if (a.cost) a.cost[b] = tc;
+    if (a.steps) a.steps[b] = steps;
+    if (a.delta) {
+      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)td0);
+      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)td1);
+    }
+    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
   }
 }
 
@@ -4358,6 +4946,54 @@ int launch_santa_vt_sc(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   return SH_OK;
 }
 
+// Dense-tile one-wave kernel + the windowed-key launch over the blocks it
+// left (out of range; every block under the exact-argmin and range test
+// flags).  Counters alternate as in launch_santa_sp.
+int launch_santa_dt(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
+  const size_t lds = dt_lds_layout(a.n, ctx->ng).total;
+  if (lds > 160 * 1024) return fail(SH_ERR_ARGS, "dense tile: too many gift types for LDS");
+  static thread_local AttrCache attr;
+  if (lds > 64 * 1024 && attr.need(ctx->device, lds)) {
+    HIP_TRY(hipFuncSetAttribute((const void *)santa_dt_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    attr.set(ctx->device, lds);
+  }
+  HIP_TRY_RC(ensure_ovf(ctx, B, s));
+  const int p = ctx->ovf_par;
+  a.ovf_cnt = ctx->d_ovf + p;
+  a.ovf_list = ctx->d_ovf + 2 + (size_t)p * ctx->ovf_cap;
+  a.blist = nullptr;
+  hipLaunchKernelGGL(santa_dt_kernel, dim3(B), dim3(SANTA_WG), lds, s, a);
+  HIP_TRY(hipGetLastError());
+  SantaArgs f = a;
+  f.blist = a.ovf_list;
+  f.bcount = a.ovf_cnt;
+  f.ovf_reset = ctx->d_ovf + (p ^ 1);
+  const int rc = launch_santa_vt<0, 0>(ctx, f, B, s);
+  if (rc) {
+    (void)hipMemsetAsync(ctx->d_ovf + p, 0, sizeof(int32_t), s);
+    return rc;
+  }
+  ctx->ovf_par = p ^ 1;
+  return SH_OK;
+}
+
+// Twins dense-tile one-wave kernel (its out-of-range blocks are re-solved in
+// the same workgroup).
+int launch_santa_dtw(sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
+  const size_t lds = dtw_lds_bytes(a.n, ctx->ng);
+  if (lds > 160 * 1024) return fail(SH_ERR_ARGS, "twins dense tile: block too large for LDS");
+  static thread_local AttrCache attr;
+  if (lds > 64 * 1024 && attr.need(ctx->device, lds)) {
+    HIP_TRY(hipFuncSetAttribute((const void *)santa_dtw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    attr.set(ctx->device, lds);
+  }
+  hipLaunchKernelGGL(santa_dtw_kernel, dim3(B), dim3(SANTA_WG), lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return SH_OK;
+}
+
 // Sparse-tile kernel + the fallback launch for blocks whose hit lists did not
 // fit.  The two overflow counters alternate between calls: the fallback
 // launch of call k resets the counter that call k+1 appends to.
@@ -4471,8 +5107,9 @@ int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   if (n > 256 || mode == SH_MODE_TRIPLETS) return SH_DESIGN_LARGE;
   // twins keep the LDS tile: their 128-dword register column does not stay
   // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
-  if (mode == SH_MODE_TWINS) return SH_DESIGN_TWINS;
+  if (mode == SH_MODE_TWINS) return (flags & SH_FLAG_DT_TILE) ? SH_DESIGN_DT_TWINS : SH_DESIGN_TWINS;
   if (flags & SH_FLAG_LDS_TILE) return SH_DESIGN_LDS_TILE;
+  if (flags & SH_FLAG_DT_TILE) return SH_DESIGN_DT_TILE;
   // (SH_FLAG_SW_TILE, the retired one-wave register-tile kernel, is refused
   // by the entry points)
   // the sparse kernel packs child ids (< 2^20) and gift types (< 1023) in one
@@ -4523,6 +5160,8 @@ int resident_blocks(sh_ctx *ctx, int design, int mode, int n, int B) {
     case SH_DESIGN_TWINS:
       return occ_blocks(ctx, santa_block_kernel<1, 1>, SANTA_WG, santa_lds_layout(n, 1, ctx->ng).total);
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
+    case SH_DESIGN_DT_TILE: return occ_blocks(ctx, santa_dt_kernel, SANTA_WG, dt_lds_layout(n, ctx->ng).total);
+    case SH_DESIGN_DT_TWINS: return occ_blocks(ctx, santa_dtw_kernel, SANTA_WG, dtw_lds_bytes(n, ctx->ng));
     case SH_DESIGN_VT_TILE: return vt_tile_slots(ctx);
     case SH_DESIGN_SPARSE3:
       return ctx->d_wish10 ? occ_blocks(ctx, santa_sp3_kernel<false, true>, WAVE, 0)
@@ -4564,6 +5203,8 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
     case SH_DESIGN_LDS_TILE:
       return (flags & SH_FLAG_TIMING) ? launch_santa<1, 0, true>(ctx, a, B, s) : launch_santa<1, 0>(ctx, a, B, s);
     case SH_DESIGN_VT_TILE: return launch_santa_vt_sc(ctx, a, B, s);
+    case SH_DESIGN_DT_TILE: return launch_santa_dt(ctx, a, B, s);
+    case SH_DESIGN_DT_TWINS: return launch_santa_dtw(ctx, a, B, s);
     case SH_DESIGN_SPARSE3: return launch_santa_sp(ctx, a, B, s, true);
     default: return launch_santa_sp(ctx, a, B, s, false);
   }

@@ -205,9 +205,10 @@ def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
         flag_sets = (0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1,
                      _lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_TEST_RANGE,
                      _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_LDS_TILE | _lib.SH_FLAG_TEST_RANGE,
-                     _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_VT_TILE | _lib.SH_FLAG_TEST_RANGE)
+                     _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_VT_TILE | _lib.SH_FLAG_TEST_RANGE,
+                     _lib.SH_FLAG_DT_TILE, _lib.SH_FLAG_DT_TILE | _lib.SH_FLAG_TEST_RANGE)
     elif mode == 1 and n <= 256:
-        flag_sets = (0, _lib.SH_FLAG_TEST_RANGE)
+        flag_sets = (0, _lib.SH_FLAG_TEST_RANGE, _lib.SH_FLAG_DT_TILE, _lib.SH_FLAG_DT_TILE | _lib.SH_FLAG_TEST_RANGE)
     else:
         flag_sets = (0,)
     for fl in flag_sets:
@@ -562,7 +563,8 @@ def test_fast_and_exact_argmin_agree(sh, ctx, full_data):
     for mode, n, B in ((0, 256, 32), (1, 256, 4)):
         rows = ctx.sample_blocks(mode, n, B, 31, 2)
         outs = []
-        extra = (_lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_EXACT_ARGMIN,) if mode == 0 else ()
+        extra = ((_lib.SH_FLAG_SP_TILE | _lib.SH_FLAG_EXACT_ARGMIN, _lib.SH_FLAG_DT_TILE | _lib.SH_FLAG_EXACT_ARGMIN)
+                 if mode == 0 else (_lib.SH_FLAG_DT_TILE, _lib.SH_FLAG_DT_TILE | _lib.SH_FLAG_EXACT_ARGMIN))
         for fl in (0, _lib.SH_FLAG_EXACT_ARGMIN) + extra:
             types = ctx.upload_types(full_data.types)
             col = torch.empty(B * n, dtype=torch.int32, device="cuda")
@@ -651,15 +653,16 @@ def test_sparse_overflow_fallback(sh, ctx, full_data, design):
 
 def test_kernel_designs_agree(sh, ctx, full_data):
     """The one-wave sparse-tile kernel (SH_FLAG_SP_TILE), the default dispatch, the 4-wave
-    register-tile kernel (SH_FLAG_VT_TILE) and the 4-wave LDS-tile kernel
-    (SH_FLAG_LDS_TILE) produce identical rounds: col, cost, deltas, steps,
-    state.  The retired one-wave register kernel's flag is refused."""
+    register-tile kernel (SH_FLAG_VT_TILE), the 4-wave LDS-tile kernel
+    (SH_FLAG_LDS_TILE) and the dense-tile one-wave kernel (SH_FLAG_DT_TILE)
+    produce identical rounds: col, cost, deltas, steps, state.  The retired one-wave register kernel's flag is refused."""
     from santa_hip import _lib
     mode = 0
     for B, nn in ((64, 256), (16, 100), (8, 37), (8, 130), (4, 1), (6, 255), (5, 64)):
         rows = ctx.sample_blocks(mode, nn, B, 77, 9)
         outs = []
-        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_SP1, _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_LDS_TILE):
+        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_SP1, _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_LDS_TILE,
+                   _lib.SH_FLAG_DT_TILE):
             types = ctx.upload_types(full_data.types)
             col = torch.empty(B * nn, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -692,7 +695,7 @@ def test_shard_designs_agree(sh, ctx, full_data):
     for B in (933, 466):
         rows = ctx.sample_blocks(0, 256, B, 2017, 0)
         outs = []
-        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_TEST_RANGE, _lib.SH_FLAG_EXACT_ARGMIN):
+        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_TEST_RANGE, _lib.SH_FLAG_EXACT_ARGMIN, _lib.SH_FLAG_DT_TILE):
             types = ctx.upload_types(full_data.types)
             col = torch.empty(B * 256, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -716,6 +719,8 @@ def test_design_dispatch(sh, ctx):
     assert ctx.solve_design(0, 256, 3730) == _lib.SH_DESIGN_SPARSE3
     assert ctx.solve_design(0, 256, 466) == 1
     assert ctx.solve_design(0, 256, 466, _lib.SH_FLAG_SP_TILE) == _lib.SH_DESIGN_SPARSE3
+    assert ctx.solve_design(0, 256, 3730, _lib.SH_FLAG_DT_TILE) == _lib.SH_DESIGN_DT_TILE
+    assert ctx.resident_blocks(0, 256, 466, _lib.SH_FLAG_DT_TILE) >= 466
     assert ctx.solve_design(0, 256, 3730, _lib.SH_FLAG_SP1) == 0
     assert ctx.solve_design(0, 256, 933) == 3
     assert ctx.resident_blocks(0, 256, 933) >= 933
@@ -723,6 +728,8 @@ def test_design_dispatch(sh, ctx):
     # the register-tile design holds a whole round at once (4 waves per SIMD)
     assert ctx.resident_blocks(0, 256, 3730) >= 3730
     assert ctx.solve_design(1, 256, 78) == 4
+    assert ctx.solve_design(1, 256, 78, _lib.SH_FLAG_DT_TILE) == _lib.SH_DESIGN_DT_TWINS
+    assert ctx.resident_blocks(1, 256, 78, _lib.SH_FLAG_DT_TILE) >= 78
     assert ctx.solve_design(0, 2000, 477) == 5
     assert ctx.solve_design(1, 3000, 6) == 5
     assert ctx.solve_design(2, 256, 6) == 5
@@ -818,7 +825,8 @@ def test_santa_edge_block_sizes_vs_oracle(sh, ctx, full_data, mode, n, B):
                                       ng=full_data.ng)
     s0 = oracle.score_sums(full_data.wish, full_data.goodkids, full_data.types)
     s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
-    for fl in ((0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1) if mode == 0 else (0,)):
+    for fl in ((0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1, _lib.SH_FLAG_DT_TILE) if mode == 0
+               else (0, _lib.SH_FLAG_DT_TILE) if mode == 1 else (0,)):
         types = ctx.upload_types(full_data.types)
         col = torch.empty(B * n, dtype=torch.int32, device="cuda")
         cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -903,8 +911,8 @@ def test_bench_launches_n_ranks(sh):
 
 
 # --------------------------------------------------------------------------- input validation
-@pytest.mark.parametrize("mode,n,fl", [(0, 256, 128), (0, 256, 256), (0, 256, 8), (0, 256, 32),
-                                       (1, 256, 0), (0, 300, 0), (1, 300, 0)])
+@pytest.mark.parametrize("mode,n,fl", [(0, 256, 128), (0, 256, 256), (0, 256, 8), (0, 256, 32), (0, 256, 4096),
+                                       (1, 256, 0), (1, 256, 4096), (0, 300, 0), (1, 300, 0)])
 def test_gift_type_out_of_range_is_flagged_not_used(sh, ctx, full_data, mode, n, fl):
     """A current gift type outside [0, ng) in a block (it would index the
     kernels' on-chip tables) makes every kernel design skip that block and
@@ -1004,7 +1012,8 @@ def test_no_apply_solves_overlapping_blocks(sh, ctx, full_data):
         C = oracle.cost_single(full_data.wish, full_data.types, r[b], ng=full_data.ng)
         _, oc = oracle.lsap(C)
         want.append((oc, int(C[np.arange(n), oc].sum())))
-    for fl in (0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1, _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_VT_TILE):
+    for fl in (0, _lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_SP1, _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_VT_TILE,
+               _lib.SH_FLAG_DT_TILE):
         types = ctx.upload_types(full_data.types)
         col = torch.empty(B * n, dtype=torch.int32, device="cuda")
         cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -1036,7 +1045,7 @@ def test_small_wishlists_match_oracle(sh, nw, ng, nq):
     r = rows.cpu().numpy().reshape(B, n)
     want_types = sd.types.copy()
     want_col, want_cost = oracle.round_blocks(0, sd.wish, want_types, r, ng=ng)
-    for fl in (_lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_VT_TILE):
+    for fl in (_lib.SH_FLAG_SP_TILE, _lib.SH_FLAG_LDS_TILE, _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_DT_TILE):
         types = c.upload_types(sd.types)
         col = torch.empty(B * n, dtype=torch.int32, device="cuda")
         cost = torch.empty(B, dtype=torch.int64, device="cuda")
