@@ -3236,7 +3236,6 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const int p0 = n - 1 - 4 * ln;
         *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
       }
-      if (lane == 0) rowq[n - 1] = ubase + 4u * (uint32_t)cur;  // (step 0's row)
       int nrem = n;
       int32_t minVal = 0;
       int i = cur;
@@ -3248,10 +3247,6 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       uint64_t wmask = 0, mmask = 0;
       int kw = 0, kmv = 0;
       uint32_t kX = 0;
-      uint32_t rpa = 0;  // the previous step's rem[pstar] address
-      // the mover: the previous step's, stored by the group, then replaced by
-      // this step's read (one register: the store reads it at issue)
-      int mover_v = 0;
       bool first = true;
       for (;;) {
         ++steps;
@@ -3272,36 +3267,34 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           stamp(tA1);
         }
         int32_t uraw;
+        int mover_v;  // the column at the last position of `remaining`
         int2 c01, c23;
         // The step's LDS traffic as one issue group for every row (a row with
         // more than 32 hits has the marker, whose slot is a dump slot, in its
-        // entry 31; such a row re-reads its columns below), no wait in between:
-        // by one lane (exec = the previous step's winner lane; none on a
-        // Dijkstra's first step) the previous step's rem[pstar] = mover and
-        // this step's row (rowq[nrem - 1] = the dual's address; step 0's is
-        // written at the set-up) -- a store of one word by all 64 lanes costs
-        // the LDS a 64-way bank conflict; then the dual and the mover, the
-        // scatter, the row reads, the un-scatter; then the previous step's
-        // book-keeping in their shadow, one lane and one register each (exec =
-        // that lane, the slot by GPR indexing on the lo tuple, %17 = its first
-        // register); one wait at the end.  Operands stay live through that wait.
+        // entry 31; such a row re-reads its columns below): the dual and the
+        // mover, the scatter, the row reads, the un-scatter, the step's row
+        // (rowq[nrem - 1] = the dual's address) -- no wait in between; then
+        // the previous step's book-keeping in their shadow, one lane and one
+        // register each (exec = that lane, the slot by GPR indexing on the lo
+        // tuple, %17 = its first register), one wait at the end.  Operands stay
+        // live through that wait.  (The one-word stores by all 64 lanes --
+        // this rowq entry, rem[pstar] after the decode -- measured 5 % faster
+        // per lone step than the same stores by one lane under an exec mask:
+        // profiles/r04_ab_stores.jsonl.)
         const uint32_t ua = ubase + 4u * (uint32_t)i;
         const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
         const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
         const int32_t miss = SP3_MISS;
         uint64_t sv;
         asm volatile(
-            "s_mov_b64 %4, exec\n\t"
-            "s_mov_b64 exec, %12\n\t"
-            "ds_write_b32 %18, %1\n\t"
-            "ds_write_b32 %7, %6 offset:1024\n\t"
-            "s_mov_b64 exec, %4\n\t"
             "ds_read_b32 %0, %6\n\t"
             "ds_read_b32 %1, %7\n\t"
             "ds_write_b32 %8, %9\n\t"
             "ds_read2_b32 %2, %10 offset1:1\n\t"
             "ds_read2_b32 %3, %10 offset0:128 offset1:129\n\t"
             "ds_write_b32 %8, %11\n\t"
+            "ds_write_b32 %7, %6 offset:1024\n\t"
+            "s_mov_b64 %4, exec\n\t"
             "s_mov_b64 exec, %12\n\t"
             "s_set_gpr_idx_on %13, gpr_idx(DST)\n\t"
             "v_mov_b32 %17, -1\n\t"
@@ -3312,9 +3305,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
             "s_set_gpr_idx_off\n\t"
             "s_mov_b64 exec, %4\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "+v"(mover_v), "=&v"(c01), "=&v"(c23), "=&s"(sv), "+v"(lo)
+            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "=&s"(sv), "+v"(lo)
             : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(miss), "s"(wmask), "s"(kw), "s"(mmask),
-              "s"(kmv), "s"(kX), "v"(lo.x), "v"(rpa)
+              "s"(kmv), "s"(kX), "v"(lo.x)
             : "memory");
         // (a row with more than 32 hits: the tile's entries and the overflow
         // list scattered again, the four columns re-read; the other half's
@@ -3375,7 +3368,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
         mmask = 1ull << (mv >> 2);
         kmv = mv & 3;
-        rpa = lds_addr(rem) + 4u * (uint32_t)pstar;  // (stored by the next step's group; a no-op when pstar == last)
+        rem[pstar] = (uint32_t)mover_v;  // (every lane, same word; a no-op when pstar == last)
         --nrem;
         // (branch-free: both the winner's column and its row are formed; the
         // row is the next step's when assigned, the column is the sink if not)
@@ -3615,7 +3608,6 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         const int p0 = n - 1 - 4 * ln;
         *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
       }
-      if (lane == 0) rowq[n - 1] = ubase + 4u * (uint32_t)cur;  // (step 0's row)
       int nrem = n;
       int32_t minVal = 0;
       int i = cur;
@@ -3623,11 +3615,10 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       uint64_t wmask = 0, mmask = 0;
       int kw = 0, kmv = 0;
       uint32_t kX = 0;
-      uint32_t rpa = 0;
-      int mover_v = 0;
       for (;;) {
         ++steps;
         int32_t uraw;
+        int mover_v;
         uint32_t w4;  // the codes of this lane's four columns in row i
         const uint32_t ua = ubase + 4u * (uint32_t)i;
         const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
@@ -3637,14 +3628,11 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         // in place of the scatter / row reads / un-scatter), the previous
         // step's book-keeping in its shadow, one wait
         asm volatile(
-            "s_mov_b64 %3, exec\n\t"
-            "s_mov_b64 exec, %9\n\t"
-            "ds_write_b32 %14, %1\n\t"
-            "ds_write_b32 %6, %5 offset:1024\n\t"
-            "s_mov_b64 exec, %3\n\t"
             "ds_read_b32 %2, %7\n\t"
             "ds_read_b32 %0, %5\n\t"
             "ds_read_b32 %1, %6\n\t"
+            "ds_write_b32 %6, %5 offset:1024\n\t"
+            "s_mov_b64 %3, exec\n\t"
             "s_mov_b64 exec, %9\n\t"
             "s_set_gpr_idx_on %10, gpr_idx(DST)\n\t"
             "v_mov_b32 %8, -1\n\t"
@@ -3655,8 +3643,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
             "s_set_gpr_idx_off\n\t"
             "s_mov_b64 exec, %3\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "+v"(mover_v), "=&v"(w4), "=&s"(sv), "+v"(lo)
-            : "v"(ua), "v"(ra), "v"(ta), "v"(lo.x), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv), "s"(kX), "v"(rpa)
+            : "=&v"(uraw), "=&v"(mover_v), "=&v"(w4), "=&s"(sv), "+v"(lo)
+            : "v"(ua), "v"(ra), "v"(ta), "v"(lo.x), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv), "s"(kX)
             : "memory");
         const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
         accU |= (uint32_t)ui + LR.CU;
@@ -3686,7 +3674,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
         mmask = 1ull << (mv >> 2);
         kmv = mv & 3;
-        rpa = lds_addr(rem) + 4u * (uint32_t)pstar;
+        rem[pstar] = (uint32_t)mover_v;  // (every lane, same word: see santa_sp3_kernel)
         --nrem;
         sink = 4 * lw + kw;
         i = __builtin_amdgcn_readlane((int)rsel, lw);
@@ -3871,7 +3859,6 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dtw_kernel(SantaArgs a) {
         const int p0 = n - 1 - 4 * ln;
         *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
       }
-      if (lane == 0) rowq[n - 1] = ubase + 8u * (uint32_t)cur;  // (step 0's row)
       int nrem = n;
       int64_t minVal = 0;
       int i = cur;
@@ -3879,25 +3866,21 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dtw_kernel(SantaArgs a) {
       uint64_t wmask = 0, mmask = 0;
       int kw = 0, kmv = 0;
       uint32_t kX = 0;
-      uint32_t rpa = 0;
-      int mover_v = 0;
       for (;;) {
         ++steps;
         uint64_t uraw;
+        int mover_v;
         uint2 e4;  // the entries of this lane's four columns in row i
         const uint32_t ua = ubase + 8u * (uint32_t)i;
         const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
         const uint32_t ta = tbase + (uint32_t)i * (2u * (uint32_t)RS);
         uint64_t sv;
         asm volatile(
-            "s_mov_b64 %3, exec\n\t"
-            "s_mov_b64 exec, %11\n\t"
-            "ds_write_b32 %16, %1\n\t"
-            "ds_write_b32 %7, %6 offset:1024\n\t"
-            "s_mov_b64 exec, %3\n\t"
             "ds_read_b64 %2, %8\n\t"
             "ds_read_b64 %0, %6\n\t"
             "ds_read_b32 %1, %7\n\t"
+            "ds_write_b32 %7, %6 offset:1024\n\t"
+            "s_mov_b64 %3, exec\n\t"
             "s_mov_b64 exec, %11\n\t"
             "s_set_gpr_idx_on %12, gpr_idx(DST)\n\t"
             "v_mov_b32 %9, -1\n\t"
@@ -3909,9 +3892,9 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dtw_kernel(SantaArgs a) {
             "s_set_gpr_idx_off\n\t"
             "s_mov_b64 exec, %3\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "+v"(mover_v), "=&v"(e4), "=&s"(sv), "+v"(lo), "+v"(hm)
+            : "=&v"(uraw), "=&v"(mover_v), "=&v"(e4), "=&s"(sv), "+v"(lo), "+v"(hm)
             : "v"(ua), "v"(ra), "v"(ta), "v"(lo.x), "v"(hm.x), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv),
-              "s"(kX), "v"(rpa)
+              "s"(kX)
             : "memory");
         const int64_t ui = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uraw >> 32)) << 32) |
                                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)uraw));
@@ -3944,7 +3927,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dtw_kernel(SantaArgs a) {
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
         mmask = 1ull << (mv >> 2);
         kmv = mv & 3;
-        rpa = lds_addr(rem) + 4u * (uint32_t)pstar;
+        rem[pstar] = (uint32_t)mover_v;  // (every lane, same word: see santa_sp3_kernel)
         --nrem;
         sink = 4 * lw + kw;
         i = __builtin_amdgcn_readlane((int)rsel, lw);
@@ -4628,6 +4611,7 @@ struct sh_ctx {
   int ovf_par = 0;
   int n_cu = 0;          // compute units (LDS-tile slot count)
   int lds_slots = 0, lds_slots_n = -1;  // cached lds_tile_slots for one n
+  int dt_slots = 0, dt_slots_n = -1;    // cached dt_tile_slots for one n
   int vt_slots = -1;                     // cached vt_tile_slots
 };
 
@@ -5091,6 +5075,22 @@ int lds_tile_slots(sh_ctx *ctx, int n) {
   return ctx->lds_slots;
 }
 
+// Dense-tile one-wave blocks (singles) the device holds at once for this n.
+int dt_tile_slots(sh_ctx *ctx, int n) {
+  if (ctx->dt_slots_n == n) return ctx->dt_slots;
+  int per_cu = 0;
+  const size_t lds = dt_lds_layout(n, ctx->ng).total;
+  if (lds <= 160 * 1024) {
+    if (lds > 64 * 1024)
+      (void)hipFuncSetAttribute((const void *)santa_dt_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, santa_dt_kernel, SANTA_WG, lds) != hipSuccess)
+      per_cu = 0;
+  }
+  ctx->dt_slots = per_cu * ctx->n_cu;
+  ctx->dt_slots_n = n;
+  return ctx->dt_slots;
+}
+
 // Register-tile 4-wave blocks (singles) the device holds at once.
 int vt_tile_slots(sh_ctx *ctx) {
   if (ctx->vt_slots >= 0) return ctx->vt_slots;
@@ -5119,16 +5119,15 @@ int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   // code reserved (n_wish <= 126); the LDS-list kernel takes the rest
   const int sparse = (ctx->n_wish > 126 || (flags & SH_FLAG_SP1)) ? SH_DESIGN_SPARSE : SH_DESIGN_SPARSE3;
   if (flags & (SH_FLAG_SP_TILE | SH_FLAG_SP1)) return sparse;
-  // few blocks (at most one resident wave of LDS-tile blocks): every block
-  // starts at once and the launch takes one block's latency, which the
-  // 4-wave tile kernel has lower (MI355X, one GPU's shard of a round at 8
-  // GPUs, 466 blocks: 2.25 vs 2.41 ms at round 0, 0.81 vs 0.95 ms at round 10)
-  if (B <= lds_tile_slots(ctx, n)) return SH_DESIGN_LDS_TILE;
-  // up to one resident wave of register-tile 4-wave blocks (4 per CU): the
-  // latency-bound shard of a round at 4 GPUs (933 blocks: 1.68 vs 2.13 ms at
-  // round 0, 0.67 vs 0.89 ms at round 10 for the sparse kernel; beyond it the
-  // sparse kernel's 4 blocks per SIMD win: 1865 blocks 2.45 vs 2.76 ms)
-  if (sparse != SH_DESIGN_SPARSE && B <= vt_tile_slots(ctx)) return SH_DESIGN_VT_TILE;
+  // few blocks (at most one resident wave of dense-tile blocks, two per CU):
+  // every block starts at once and the launch takes one block's latency,
+  // which the one-wave dense-tile kernel has lowest (round 4, MI355X, one
+  // GPU's shard of a round at 8 GPUs, 466 blocks: 1.13 ms at round 0 against
+  // 1.36 for the 4-wave LDS tile and 1.45 for the sparse kernel, 0.49 / 0.52
+  // / 0.65 ms at round 10; profiles/r04_shard_dt.jsonl).  Beyond it the
+  // sparse kernel: at 933 blocks (the shard at 4 GPUs) 1.52 ms against 1.60
+  // for the 4-wave register tile and 1.76 for two waves of dense-tile blocks.
+  if (ctx->n_wish <= 254 && B <= dt_tile_slots(ctx, n)) return SH_DESIGN_DT_TILE;
   return sparse;
 }
 
@@ -5160,7 +5159,7 @@ int resident_blocks(sh_ctx *ctx, int design, int mode, int n, int B) {
     case SH_DESIGN_TWINS:
       return occ_blocks(ctx, santa_block_kernel<1, 1>, SANTA_WG, santa_lds_layout(n, 1, ctx->ng).total);
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
-    case SH_DESIGN_DT_TILE: return occ_blocks(ctx, santa_dt_kernel, SANTA_WG, dt_lds_layout(n, ctx->ng).total);
+    case SH_DESIGN_DT_TILE: return dt_tile_slots(ctx, n);
     case SH_DESIGN_DT_TWINS: return occ_blocks(ctx, santa_dtw_kernel, SANTA_WG, dtw_lds_bytes(n, ctx->ng));
     case SH_DESIGN_VT_TILE: return vt_tile_slots(ctx);
     case SH_DESIGN_SPARSE3:

@@ -687,15 +687,17 @@ def test_kernel_designs_agree(sh, ctx, full_data):
 
 
 def test_shard_designs_agree(sh, ctx, full_data):
-    """One GPU's shard of a round at 4 and 8 GPUs (933 / 466 blocks, the
-    register-tile and LDS-tile 4-wave kernels by default) equals the
-    register-tile sparse kernel's result, also with every block sent through
-    the windowed-key re-solve (SH_FLAG_TEST_RANGE) and the exact argmin."""
+    """One GPU's shard of a round at 4 and 8 GPUs (933 / 466 blocks: the
+    sparse and the dense-tile kernels by default) equals the sparse kernel's
+    result, also with every block sent through the windowed-key re-solve
+    (SH_FLAG_TEST_RANGE) and the exact argmin, and on the dense-tile, 4-wave
+    register-tile and 4-wave LDS-tile kernels."""
     from santa_hip import _lib
     for B in (933, 466):
         rows = ctx.sample_blocks(0, 256, B, 2017, 0)
         outs = []
-        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_TEST_RANGE, _lib.SH_FLAG_EXACT_ARGMIN, _lib.SH_FLAG_DT_TILE):
+        for fl in (_lib.SH_FLAG_SP_TILE, 0, _lib.SH_FLAG_TEST_RANGE, _lib.SH_FLAG_EXACT_ARGMIN, _lib.SH_FLAG_DT_TILE,
+                   _lib.SH_FLAG_VT_TILE, _lib.SH_FLAG_LDS_TILE):
             types = ctx.upload_types(full_data.types)
             col = torch.empty(B * 256, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -710,19 +712,21 @@ def test_shard_designs_agree(sh, ctx, full_data):
 
 
 def test_design_dispatch(sh, ctx):
-    """Singles n=256: the sparse kernel for a full round (3730 blocks), the
-    4-wave LDS tile when the launch fits in one resident wave of LDS-tile
-    blocks (one GPU's shard at 8 GPUs: 466), the 4-wave register tile when it
-    fits in one resident wave of those (the shard at 4 GPUs: 933), the sparse
-    kernel again when forced; twins and large blocks have one design each."""
+    """Singles n=256: the sparse kernel for a full round (3730 blocks) and for
+    the shards at 2 and 4 GPUs (1865, 933), the dense-tile one-wave kernel
+    when the launch fits in one resident wave of its blocks (one GPU's shard
+    at 8 GPUs: 466), the sparse kernel again when forced; twins and large
+    blocks have one default design each."""
     from santa_hip import _lib
     assert ctx.solve_design(0, 256, 3730) == _lib.SH_DESIGN_SPARSE3
-    assert ctx.solve_design(0, 256, 466) == 1
+    assert ctx.solve_design(0, 256, 466) == _lib.SH_DESIGN_DT_TILE
+    assert ctx.resident_blocks(0, 256, 466) >= 466
     assert ctx.solve_design(0, 256, 466, _lib.SH_FLAG_SP_TILE) == _lib.SH_DESIGN_SPARSE3
     assert ctx.solve_design(0, 256, 3730, _lib.SH_FLAG_DT_TILE) == _lib.SH_DESIGN_DT_TILE
     assert ctx.resident_blocks(0, 256, 466, _lib.SH_FLAG_DT_TILE) >= 466
     assert ctx.solve_design(0, 256, 3730, _lib.SH_FLAG_SP1) == 0
-    assert ctx.solve_design(0, 256, 933) == 3
+    assert ctx.solve_design(0, 256, 933) == _lib.SH_DESIGN_SPARSE3
+    assert ctx.solve_design(0, 256, 933, _lib.SH_FLAG_VT_TILE) == 3
     assert ctx.resident_blocks(0, 256, 933) >= 933
     assert ctx.solve_design(0, 256, 1865) == _lib.SH_DESIGN_SPARSE3
     # the register-tile design holds a whole round at once (4 waves per SIMD)
