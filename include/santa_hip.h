@@ -73,11 +73,10 @@ extern "C" {
                                    one-wave kernel (santa_sp2_kernel) left
                                    the library; every entry point returns
                                    SH_ERR_ARGS for this flag               */
-#define SH_FLAG_DT_TILE 4096u   /* force the dense-tile one-wave kernels
-                                   (4 waves build the LDS tile, one wave
-                                   solves: santa_dt_kernel for singles,
-                                   santa_dtw_kernel for twins, n <= 256;
-                                   identical results)                      */
+#define SH_FLAG_DT_TILE 4096u   /* force the dense-tile one-wave kernel
+                                   (santa_dt_kernel: 4 waves build the LDS
+                                   byte tile, one wave solves; singles,
+                                   n <= 256; identical results)            */
 #define SH_FLAG_NO_APPLY 1024u  /* solve and report (col, cost, deltas,
                                    steps) but leave the gift types untouched:
                                    blocks may then overlap (batched
@@ -95,8 +94,6 @@ extern "C" {
                                 32-bit lattice keys (full rounds, default)  */
 #define SH_DESIGN_DT_TILE 8  /* byte tile in LDS built by 4 waves, solved by
                                 one wave, 32-bit lattice keys (few blocks)  */
-#define SH_DESIGN_DT_TWINS 9 /* twins: code-pair tile in LDS built by 4
-                                waves, solved by one wave, 64-bit keys      */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024

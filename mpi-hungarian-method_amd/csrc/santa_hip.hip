@@ -345,6 +345,18 @@ __device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
+// Inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8 inside
+// each row of 16, then row_bcast 15/31 across rows).
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
 // 32-bit unsigned min within each 16-lane row, held by every lane of the row
 __device__ __forceinline__ uint32_t row_min_u32_dpp(uint32_t x) {
   x = dpp_min_step<0xB1, 0xF>(x);   // quad_perm [1,0,3,2]
@@ -1292,6 +1304,133 @@ __device__ __forceinline__ bool lds_tile_build(const SantaArgs &a, const int b, 
   return true;
 }
 
+// The dense tile build from the packed wishlists (one 128-byte line per
+// child), for santa_dt_kernel (MODE 0: uint8 codes, row stride RS bytes) and
+// the 4-wave twins kernel (MODE 1: code pairs, twin k's code in byte k of the
+// uint16 entry, row stride RS entries): the columns counting-sorted by gift
+// type into a type table (santa_sp3_kernel's: a type's first two columns, its
+// third or its start in the sorted column list, its count), then thread R
+// builds row R alone in wish order (twins: both twins' wishlists) -- per wish
+// one table read and the rank code written at the type's first two columns
+// (this thread's dump byte when the type has fewer), the rest of a larger
+// type from the sorted list behind a wave-uniform test.  Against
+// lds_tile_build's type -> column chains walked per wish, ~10x fewer LDS
+// round trips.  false: the block's rows or types are bad (error flag set),
+// or a type has 255+ of the block's columns (decline: the caller builds with
+// lds_tile_build instead).  All SANTA_WG threads call it; n <= SANTA_WG;
+// gift ids < FAST_MAX_NG (10-bit packed rows).
+constexpr int FAST_MAX_NG = 1024;
+template <int MODE>
+__device__ __forceinline__ bool fast_tile_build(const SantaArgs &a, const int b, const int n, const int RS,
+                                                uint8_t *tile8, int32_t *rows_l, int16_t *ctype, uint32_t *thead,
+                                                uint8_t *csort, uint32_t *wsum, uint8_t *dump, bool &decline) {
+  const int tid = threadIdx.x, j = tid;
+  decline = false;
+  const bool live = j < n;
+  const int child = live ? a.rows[(size_t)b * n + j] : 0;
+  if (__syncthreads_or(live && (child < 0 || child + MODE >= a.nc))) {
+    if (tid == 0) atomicOr(a.err, SH_ERRF_ROWS);
+    return false;
+  }
+  // the row's packed wishlist lines (twins: both twins'), in flight during the sort
+  uint4 G4[8 * (MODE + 1)];
+#pragma unroll
+  for (int k = 0; k <= MODE; ++k)
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      G4[8 * k + q] = live ? ((const uint4 *)(a.wish10 + (size_t)(child + k) * 32))[q] : make_uint4(0, 0, 0, 0);
+  const int ty = live ? (int)a.types[child] : -1;
+  if (live) {
+    rows_l[j] = child;
+    ctype[j] = (int16_t)ty;
+  }
+  for (int t = tid; t < a.ng; t += SANTA_WG) thead[t] = 0u;
+  {  // zero the tile
+    uint4 *t4 = (uint4 *)tile8;
+    const int n16 = (int)((size_t)n * RS * (MODE + 1) / 16);
+    for (int q = tid; q < n16; q += SANTA_WG) t4[q] = make_uint4(0, 0, 0, 0);
+  }
+  if (__syncthreads_or(live && (ty < 0 || ty >= a.ng))) {
+    if (tid == 0) atomicOr(a.err, SH_ERRF_TYPE);
+    return false;
+  }
+  if (live) atomicAdd(&thead[ty], 1u << 16);
+  __syncthreads();
+  {  // exclusive scan of the counts over types -> start of each type in csort
+    const int per = (a.ng + SANTA_WG - 1) / SANTA_WG;
+    const int t0 = tid * per, t1 = min(a.ng, t0 + per);
+    uint32_t sum = 0;
+    int big = 0;
+    for (int t = t0; t < t1; ++t) {
+      const uint32_t c = thead[t] >> 16;
+      sum += c;
+      big |= c >= 255u;
+    }
+    const uint32_t incl = wave_incl_scan_u32(sum);
+    if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+    if (__syncthreads_or(big)) {
+      decline = true;
+      return false;
+    }
+    uint32_t run = incl - sum;
+    for (int w = 0; w < (tid >> 6); ++w) run += wsum[w];
+    for (int t = t0; t < t1; ++t) {
+      const uint32_t h = thead[t];
+      thead[t] = h | run;  // low half: fill cursor
+      run += h >> 16;
+    }
+  }
+  __syncthreads();
+  if (live) csort[atomicAdd(&thead[ty], 1u) & 0xFFFFu] = (uint8_t)j;
+  __syncthreads();
+  for (int t = tid; t < a.ng; t += SANTA_WG) {
+    const uint32_t h = thead[t];
+    const uint32_t c = h >> 16, e = (h & 0xFFFFu) - c;
+    const uint32_t x2 = c <= 3u ? (uint32_t)csort[e + 2] : e;
+    thead[t] = c ? ((uint32_t)csort[e] | ((uint32_t)csort[e + 1] << 8) | (x2 << 16) | (c << 24)) : 0u;
+  }
+  __syncthreads();
+  if (live) {
+    const int nw = a.n_wish;
+#pragma unroll
+    for (int k = 0; k <= MODE; ++k) {
+      uint32_t G[32];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        G[4 * q] = G4[8 * k + q].x;
+        G[4 * q + 1] = G4[8 * k + q].y;
+        G[4 * q + 2] = G4[8 * k + q].z;
+        G[4 * q + 3] = G4[8 * k + q].w;
+      }
+      // column col of row j, twin k: byte ((j * RS + col) << MODE) + k
+      uint8_t *row = tile8 + (((size_t)j * RS) << MODE) + k;
+#pragma unroll
+      for (int r = 0; r < 104; ++r) {  // (n_wish <= 102 for the packed copy)
+        if (r < nw) {
+          const int bit = 10 * r;
+          const uint32_t w0 = G[(bit >> 5) & 31], w1 = G[((bit >> 5) + 1) & 31];
+          const int g = (int)(__builtin_amdgcn_alignbit(w1, w0, bit & 31) & 1023u);
+          const uint32_t h = thead[g];
+          const uint32_t cg = h >> 24;
+          const uint8_t code = (uint8_t)(r + 1);
+          *(cg >= 1 ? row + ((h & 0xFFu) << MODE) : dump) = code;
+          *(cg >= 2 ? row + (((h >> 8) & 0xFFu) << MODE) : dump) = code;
+          if (__builtin_expect(__any(cg >= 3), 0)) {
+            if (cg == 3) {
+              row[((h >> 16) & 0xFFu) << MODE] = code;
+            } else if (cg >= 4) {
+              const uint32_t e = (h >> 16) & 0xFFu;
+              for (uint32_t m = 2; m < cg; ++m) row[(uint32_t)csort[e + m] << MODE] = code;
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  return true;
+}
+
 template <int K, int MODE, bool TIMED = false>
 __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   static_assert(K == 1, "one column per thread (n <= 256)");
@@ -1310,7 +1449,19 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   SolveLds S{(int64_t *)(smem + L.u), (int16_t *)(smem + L.c4r), (int16_t *)(smem + L.r4c),
              (int16_t *)(smem + L.path), (uint64_t *)(smem + L.red)};
 
-  if (!lds_tile_build<MODE>(a, b, n, RS, tile8, rows_l, ctype, head, nxt)) return;
+  {
+    // twins with the packed wishlists: the fast build (type table in the
+    // chain heads' place, the column sort in the links', dump bytes in the
+    // step words', four scan words in the partials'), else / when it
+    // declines the type -> column chains.  (Singles here are the forced
+    // SH_FLAG_LDS_TILE design: the chains.)
+    bool decline = MODE == 0 || a.wish10 == nullptr || a.ng > FAST_MAX_NG;
+    if (!decline && !fast_tile_build<MODE>(a, b, n, RS, tile8, rows_l, ctype, (uint32_t *)head, (uint8_t *)nxt,
+                                           (uint32_t *)part, (uint8_t *)S.red + tid, decline) &&
+        !decline)
+      return;
+    if (decline && !lds_tile_build<MODE>(a, b, n, RS, tile8, rows_l, ctype, head, nxt)) return;
+  }
   for (int i = tid; i < n; i += SANTA_WG) {
     S.u[i] = 0;
     S.c4r[i] = -1;
@@ -1895,17 +2046,6 @@ __host__ __device__ __forceinline__ SpLds sp_lds_layout(int ng, int cap) {
   return L;
 }
 
-// Inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8 inside
-// each row of 16, then row_bcast 15/31 across rows).
-__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
-  return x;
-}
 
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
 
@@ -3529,7 +3669,7 @@ struct DtLds {
 __host__ __device__ __forceinline__ DtLds dt_lds_layout(int n, int ng) {
   DtLds L;
   size_t off = 0;
-  L.tile = off;  off += (size_t)n * DT_RS;
+  L.tile = off;  off += (size_t)(n + 1) * DT_RS;  // (+ a dump row for the fast build)
   L.u = off;     off += (256 + 64) * 4;  // row duals (int32) + a dump slot per lane
   L.rows = off;  off += r16((size_t)n * 4);
   L.ctype = off; off += r16((size_t)n * 2);
@@ -3551,9 +3691,21 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
   int32_t *rows_l = (int32_t *)(smem + L.rows);
   int16_t *ctype = (int16_t *)(smem + L.ctype);
   uint32_t *rem = (uint32_t *)(smem + L.rem);
-  if (!lds_tile_build<0>(a, b, n, DT_RS, tile8, rows_l, ctype, (int32_t *)(smem + L.head),
-                         (int16_t *)(smem + L.nxt)))
-    return;
+  {
+    // the packed wishlists: the fast build (thead in the chain heads' place,
+    // the column sort in the chain links', four scan words in the duals'),
+    // else / when it declines the type -> column chains
+    bool decline = a.wish10 == nullptr || a.ng > FAST_MAX_NG;
+    if (!decline &&
+        !fast_tile_build<0>(a, b, n, DT_RS, tile8, rows_l, ctype, (uint32_t *)(smem + L.head), smem + L.nxt,
+                            (uint32_t *)(smem + L.u), tile8 + (size_t)n * DT_RS + tid, decline) &&
+        !decline)
+      return;
+    if (decline &&
+        !lds_tile_build<0>(a, b, n, DT_RS, tile8, rows_l, ctype, (int32_t *)(smem + L.head),
+                           (int16_t *)(smem + L.nxt)))
+      return;
+  }
   __syncthreads();
   if (tid >= WAVE) return;  // (wave 0 solves; no barrier from here on)
   const int lane = tid;
@@ -3608,6 +3760,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         const int p0 = n - 1 - 4 * ln;
         *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
       }
+      if (lane == 0) rowq[n - 1] = ubase + 4u * (uint32_t)cur;  // (step 0's row)
       int nrem = n;
       int32_t minVal = 0;
       int i = cur;
@@ -3615,10 +3768,11 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       uint64_t wmask = 0, mmask = 0;
       int kw = 0, kmv = 0;
       uint32_t kX = 0;
+      uint32_t rpa = 0;   // the previous step's rem[pstar] address
+      int mover_v = 0;    // its mover, stored by the group, then replaced by this step's
       for (;;) {
         ++steps;
         int32_t uraw;
-        int mover_v;
         uint32_t w4;  // the codes of this lane's four columns in row i
         const uint32_t ua = ubase + 4u * (uint32_t)i;
         const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
@@ -3626,13 +3780,21 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         uint64_t sv;
         // the step's LDS group (santa_sp3_kernel's, with the tile row read
         // in place of the scatter / row reads / un-scatter), the previous
-        // step's book-keeping in its shadow, one wait
+        // step's book-keeping in its shadow, one wait.  Here the one-word
+        // stores (the previous step's rem[pstar] = mover, this step's rowq
+        // entry) go by one lane (exec = the previous winner's lane; none on a
+        // Dijkstra's first step, whose row the set-up stores): 2 % faster per
+        // lone step than by all 64 lanes, the reverse of santa_sp3_kernel
+        // (profiles/r04_ab_dt_stores.jsonl, r04_ab_stores.jsonl)
         asm volatile(
+            "s_mov_b64 %3, exec\n\t"
+            "s_mov_b64 exec, %9\n\t"
+            "ds_write_b32 %14, %1\n\t"
+            "ds_write_b32 %6, %5 offset:1024\n\t"
+            "s_mov_b64 exec, %3\n\t"
             "ds_read_b32 %2, %7\n\t"
             "ds_read_b32 %0, %5\n\t"
             "ds_read_b32 %1, %6\n\t"
-            "ds_write_b32 %6, %5 offset:1024\n\t"
-            "s_mov_b64 %3, exec\n\t"
             "s_mov_b64 exec, %9\n\t"
             "s_set_gpr_idx_on %10, gpr_idx(DST)\n\t"
             "v_mov_b32 %8, -1\n\t"
@@ -3643,8 +3805,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
             "s_set_gpr_idx_off\n\t"
             "s_mov_b64 exec, %3\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "=&v"(mover_v), "=&v"(w4), "=&s"(sv), "+v"(lo)
-            : "v"(ua), "v"(ra), "v"(ta), "v"(lo.x), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv), "s"(kX)
+            : "=&v"(uraw), "+v"(mover_v), "=&v"(w4), "=&s"(sv), "+v"(lo)
+            : "v"(ua), "v"(ra), "v"(ta), "v"(lo.x), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv), "s"(kX), "v"(rpa)
             : "memory");
         const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
         accU |= (uint32_t)ui + LR.CU;
@@ -3674,7 +3836,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
         mmask = 1ull << (mv >> 2);
         kmv = mv & 3;
-        rem[pstar] = (uint32_t)mover_v;  // (every lane, same word: see santa_sp3_kernel)
+        rpa = lds_addr(rem) + 4u * (uint32_t)pstar;  // (stored by the next step's group)
         --nrem;
         sink = 4 * lw + kw;
         i = __builtin_amdgcn_readlane((int)rsel, lw);
@@ -3760,300 +3922,6 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
       atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
     }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// santa_dtw_kernel (round 4): twins blocks (n <= 256 pairs; a round has 78,
-// one per CU) with santa_dt_kernel's plan in 64-bit scaled units.  Four waves
-// build the uint16 code-pair tile (lds_tile_build<1> + the twin_entry
-// re-code) as santa_block_kernel<1, 1>; then wave 0 alone solves with four
-// columns per lane, keys of sap_solve_mw_sc (every value x 2^SC_SH, so
-// sbp = spc + SC_BIAS has 17 zero low bits: the Dijkstra step t of the
-// column's last improvement sits in the low byte, as in santa_sp3_kernel)
-// and a two-word DPP argmin (high words, then the low words of the lanes at
-// the minimum), no cross-wave exchange.  A block outside the scaled range
-// (or under SH_FLAG_TEST_RANGE / SH_FLAG_EXACT_ARGMIN) is re-solved by all
-// four waves with the windowed-key solver, as santa_block_kernel does.
-// ---------------------------------------------------------------------------
-// the 4-wave twins layout + `remaining` / rows by step (512 x 4 B), the
-// one-wave solve's row duals (320 x 8 B) and two flag words
-__host__ __device__ __forceinline__ size_t dtw_lds_bytes(int n, int ng) {
-  return santa_lds_layout(n, 1, ng).total + 512 * 4 + 320 * 8 + 16;
-}
-
-__global__ __launch_bounds__(SANTA_WG) void santa_dtw_kernel(SantaArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int n = a.n;
-  const SantaLds L = santa_lds_layout(n, 1, a.ng);
-  const int RS = L.RS;
-  uint8_t *tile8 = smem + L.tile;
-  int32_t *rows_l = (int32_t *)(smem + L.rows);
-  int16_t *ctype = (int16_t *)(smem + L.ctype);
-  int64_t *part = (int64_t *)(smem + L.part);
-  SolveLds S{(int64_t *)(smem + L.u), (int16_t *)(smem + L.c4r), (int16_t *)(smem + L.r4c),
-             (int16_t *)(smem + L.path), (uint64_t *)(smem + L.red)};
-  uint32_t *rem = (uint32_t *)(smem + L.total);               // [512]: remaining, rows by step
-  int64_t *u_l = (int64_t *)(smem + L.total + 512 * 4);        // [256 + 64]: row duals + dumps
-  int32_t *flag = (int32_t *)(smem + L.total + 512 * 4 + 320 * 8);  // [2]: redo, steps
-  if (!lds_tile_build<1>(a, b, n, RS, tile8, rows_l, ctype, (int32_t *)(smem + L.head), (int16_t *)(smem + L.nxt)))
-    return;
-  const int nw1 = a.n_wish + 1;
-  const uint32_t E32 = (uint32_t)a.E;
-  __syncthreads();  // (the build's last code pairs)
-  {
-    uint4 *t4 = (uint4 *)tile8;
-    const int cnt4 = n * RS / 8;
-    auto rc2 = [&](uint32_t w) -> uint32_t {
-      return twin_entry(w & 0xFFFFu, nw1, a.E) | (twin_entry(w >> 16, nw1, a.E) << 16);
-    };
-    for (int q = tid; q < cnt4; q += SANTA_WG) {
-      const uint4 v = t4[q];
-      t4[q] = make_uint4(rc2(v.x), rc2(v.y), rc2(v.z), rc2(v.w));
-    }
-  }
-  for (int i = tid; i < n; i += SANTA_WG) {
-    S.u[i] = 0;
-    S.c4r[i] = -1;
-    S.r4c[i] = -1;
-  }
-  for (int r = tid; r < 256 + 64; r += SANTA_WG) u_l[r] = 0;
-  const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
-  const bool build_only = (a.flags & SH_FLAG_BUILD_ONLY) != 0;
-  bool redo = exact || (a.flags & SH_FLAG_TEST_RANGE) != 0;
-  __syncthreads();
-  if (tid < WAVE && !redo && !build_only) {
-    const int lane = tid;
-    uint64_t sbp[4];
-    int64_t W[4];
-    u32x4 lo, hm;  // tie bits; hm: ~0 once the column left `remaining` (the key's high word)
-    uint32_t c4r = ~0u, r4c = 0;
-    uint64_t AM[4];
-    uint32_t P[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      W[k] = 0;
-      AM[k] = 0;
-      const int j = 4 * lane + k;
-      P[k] = j < n ? ((uint32_t)(n - 1 - j) << 2) | (uint32_t)k : ~0x3FCu;
-    }
-    uint32_t *rowq = rem + 256;
-    const uint32_t ubase = lds_addr(u_l);
-    const uint32_t tbase = lds_addr(tile8) + 8u * (uint32_t)lane;
-    int steps = 0;
-    bool big = false;
-    __builtin_amdgcn_s_setprio(3);
-    for (int cur = 0; cur < n; ++cur) {
-      int ln = lane;
-      asm volatile("" : "+v"(ln));
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool asg = __builtin_amdgcn_inverse_ballot_w64(AM[k]);
-        lo[k] = P[k] ^ (asg ? 0x400u : 0x3FCu);
-        hm[k] = (4 * ln + k < n) ? 0u : ~0u;
-        sbp[k] = ~0ull;
-      }
-      {
-        const int p0 = n - 1 - 4 * ln;
-        *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
-      }
-      int nrem = n;
-      int64_t minVal = 0;
-      int i = cur;
-      int sink;
-      uint64_t wmask = 0, mmask = 0;
-      int kw = 0, kmv = 0;
-      uint32_t kX = 0;
-      for (;;) {
-        ++steps;
-        uint64_t uraw;
-        int mover_v;
-        uint2 e4;  // the entries of this lane's four columns in row i
-        const uint32_t ua = ubase + 8u * (uint32_t)i;
-        const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
-        const uint32_t ta = tbase + (uint32_t)i * (2u * (uint32_t)RS);
-        uint64_t sv;
-        asm volatile(
-            "ds_read_b64 %2, %8\n\t"
-            "ds_read_b64 %0, %6\n\t"
-            "ds_read_b32 %1, %7\n\t"
-            "ds_write_b32 %7, %6 offset:1024\n\t"
-            "s_mov_b64 %3, exec\n\t"
-            "s_mov_b64 exec, %11\n\t"
-            "s_set_gpr_idx_on %12, gpr_idx(DST)\n\t"
-            "v_mov_b32 %9, -1\n\t"
-            "v_mov_b32 %10, -1\n\t"
-            "s_set_gpr_idx_off\n\t"
-            "s_mov_b64 exec, %13\n\t"
-            "s_set_gpr_idx_on %14, gpr_idx(SRC1,DST)\n\t"
-            "v_xor_b32 %9, %15, %9\n\t"
-            "s_set_gpr_idx_off\n\t"
-            "s_mov_b64 exec, %3\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "=&v"(mover_v), "=&v"(e4), "=&s"(sv), "+v"(lo), "+v"(hm)
-            : "v"(ua), "v"(ra), "v"(ta), "v"(lo.x), "v"(hm.x), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv),
-              "s"(kX)
-            : "memory");
-        const int64_t ui = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uraw >> 32)) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)uraw));
-        uint64_t bse = SC_BIAS - (uint64_t)(ui - minVal) + (uint64_t)(n - nrem);
-        asm volatile("" : "+s"(bse));
-        const uint32_t ent[4] = {e4.x & 0xFFFFu, e4.x >> 16, e4.y & 0xFFFFu, e4.y >> 16};
-        uint32_t bh = ~0u, bl = ~0u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint64_t r = (uint64_t)W[k] + (uint64_t)twin_entry_cost<SC_SH>(ent[k], E32) + bse;
-          sbp[k] = r < sbp[k] ? r : sbp[k];
-          const uint32_t kh = (uint32_t)(sbp[k] >> 32) | hm[k];
-          const uint32_t kl = ((uint32_t)sbp[k] & ~SC_TIE_MASK) | lo[k];
-          const bool lt = kh < bh || (kh == bh && kl < bl);
-          bh = lt ? kh : bh;
-          bl = lt ? kl : bl;
-        }
-        const uint32_t rsel = __builtin_amdgcn_ubfe(r4c, bl << 3, 8);
-        const uint32_t gh = wave_min_u32_dpp(bh);
-        const uint32_t gl = wave_min_u32_dpp(bh == gh ? bl : ~0u);
-        minVal = (int64_t)((((uint64_t)gh << 32) | (gl & ~SC_TIE_MASK)) - SC_BIAS);
-        kw = (int)(gl & 3u);
-        const uint32_t pkey = (gl >> 2) & 255u;
-        const bool assigned = (gl >> 10) & 1u;
-        const int lw = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(bh == gh && bl == gl));
-        const int pstar = assigned ? (int)pkey : 255 - (int)pkey;
-        const int last = nrem - 1;
-        kX = (uint32_t)(last ^ pstar) << 2;
-        wmask = 1ull << lw;
-        const int mv = __builtin_amdgcn_readfirstlane(mover_v);
-        mmask = 1ull << (mv >> 2);
-        kmv = mv & 3;
-        rem[pstar] = (uint32_t)mover_v;  // (every lane, same word: see santa_sp3_kernel)
-        --nrem;
-        sink = 4 * lw + kw;
-        i = __builtin_amdgcn_readlane((int)rsel, lw);
-        if (!assigned) break;
-      }
-      big |= (uint64_t)(minVal + SC_LIM) >= 2 * (uint64_t)SC_LIM;
-      i32x4 prow;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
-        const int64_t dd = vk ? minVal - (int64_t)((sbp[k] & ~(uint64_t)SC_TIE_MASK) - SC_BIAS) : 0;
-        W[k] += dd;
-        const int ua = vk ? (int)((r4c >> (8 * k)) & 0xFFu) : 256 + lane;
-        __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
-      }
-      if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) AM[k] |= ((sink & 3) == k) ? 1ull << (sink >> 2) : 0ull;
-      int j = sink, pi = -1;
-      for (int hop = 0; hop <= n; ++hop) {
-        const int jl = j >> 2;
-        int pv;
-        asm volatile(
-            "s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\t"
-            "v_mov_b32 %0, %2\n\t"
-            "s_set_gpr_idx_off"
-            : "=v"(pv)
-            : "s"(j & 3), "v"(prow.x), "v"(prow));
-        const int pa = __builtin_amdgcn_readlane(pv, jl);
-        pi = (int)(((uint32_t)pa - ubase) >> 3);
-        const int pl = pi >> 2, ps = 8 * (pi & 3);
-        const uint32_t cw = (uint32_t)__builtin_amdgcn_readlane((int)c4r, pl);
-        const int t = (int)((cw >> ps) & 0xFFu);
-        const uint32_t nw4 = (cw & ~(0xFFu << ps)) | ((uint32_t)j << ps);
-        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(c4r) : "s"(nw4), "{m0}"(pl));
-        const int js = 8 * (j & 3);
-        const uint32_t rw = (uint32_t)__builtin_amdgcn_readlane((int)r4c, jl);
-        const uint32_t nr4 = (rw & ~(0xFFu << js)) | ((uint32_t)pi << js);
-        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r4c) : "s"(nr4), "{m0}"(jl));
-        j = t;
-        if (pi == cur) break;
-      }
-      big |= pi != cur;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      big |= (uint64_t)(W[k] + SC_LIM) >= 2 * (uint64_t)SC_LIM;
-      if (4 * lane + k < n) big |= (uint64_t)(u_l[4 * lane + k] + SC_LIM) >= 2 * (uint64_t)SC_LIM;
-    }
-    const bool any_big = __any(big);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (4 * lane + k < n) S.c4r[4 * lane + k] = (int16_t)((c4r >> (8 * k)) & 0xFFu);
-    if (lane == 0) {
-      flag[0] = any_big ? 1 : 0;
-      flag[1] = steps;
-    }
-  }
-  __syncthreads();
-  int64_t steps = 0;
-  int fallbacks = 0;
-  if (!redo && !build_only) {
-    redo = flag[0] != 0;
-    steps = flag[1];
-  }
-  if (build_only) {
-    for (int i = tid; i < n; i += SANTA_WG) S.c4r[i] = (int16_t)i;
-    __syncthreads();
-  } else if (redo) {  // (block-uniform) the windowed-key solver, all four waves
-    for (int i = tid; i < n; i += SANTA_WG) {
-      S.u[i] = 0;
-      S.c4r[i] = -1;
-      S.r4c[i] = -1;
-    }
-    __syncthreads();
-    const TileU16Loader<SANTA_NW, 1> ld{(const uint16_t *)tile8, E32, RS};
-    sap_solve_mw<SANTA_NW, 1>(n, ld, S, steps, fallbacks, exact);
-  }
-  // -- outputs (santa_block_kernel<1, 1>'s) --------------------------------------
-  int64_t cost = 0, dch = 0, dgh = 0;
-  for (int i = tid; i < n; i += SANTA_WG) {
-    const int col = S.c4r[i];
-    if (a.col) a.col[(size_t)b * n + i] = col;
-    const int told = ctype[i], tnew = ctype[col];
-    const int child = rows_l[i];
-    const uint16_t *t16 = (const uint16_t *)tile8;
-    const uint32_t cn = t16[(size_t)i * RS + col];
-    const uint32_t co = t16[(size_t)i * RS + i];
-    cost += twin_entry_cost<0>(cn, E32);
-    dch += twin_entry_happy(cn) - twin_entry_happy(co);
-    if (a.delta)
-      dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) - gift_happy(a, child, told) -
-             gift_happy(a, child + 1, told);
-  }
-  cost = wave_sum_i64(cost);
-  dch = wave_sum_i64(dch);
-  dgh = wave_sum_i64(dgh);
-  const int w = tid >> 6;
-  if ((tid & 63) == 0) {
-    part[3 * w + 0] = cost;
-    part[3 * w + 1] = dch;
-    part[3 * w + 2] = dgh;
-  }
-  for (int i = tid; i < n; i += SANTA_WG) {
-    const int16_t tnew = ctype[S.c4r[i]];
-    if (!(a.flags & SH_FLAG_NO_APPLY)) {
-      a.types[rows_l[i]] = tnew;
-      a.types[rows_l[i] + 1] = tnew;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int64_t tc = 0, td0 = 0, td1 = 0;
-    for (int q = 0; q < SANTA_NW; ++q) {
-      tc += part[3 * q];
-      td0 += part[3 * q + 1];
-      td1 += part[3 * q + 2];
-    }
-    if (a.cost) a.cost[b] = tc;
-    if (a.steps) a.steps[b] = steps;
-    if (a.delta) {
-      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)td0);
-      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)td1);
-    }
-    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
   }
 }
 
@@ -4962,22 +4830,6 @@ int launch_santa_dt(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   return SH_OK;
 }
 
-// Twins dense-tile one-wave kernel (its out-of-range blocks are re-solved in
-// the same workgroup).
-int launch_santa_dtw(sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
-  const size_t lds = dtw_lds_bytes(a.n, ctx->ng);
-  if (lds > 160 * 1024) return fail(SH_ERR_ARGS, "twins dense tile: block too large for LDS");
-  static thread_local AttrCache attr;
-  if (lds > 64 * 1024 && attr.need(ctx->device, lds)) {
-    HIP_TRY(hipFuncSetAttribute((const void *)santa_dtw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds));
-    attr.set(ctx->device, lds);
-  }
-  hipLaunchKernelGGL(santa_dtw_kernel, dim3(B), dim3(SANTA_WG), lds, s, a);
-  HIP_TRY(hipGetLastError());
-  return SH_OK;
-}
-
 // Sparse-tile kernel + the fallback launch for blocks whose hit lists did not
 // fit.  The two overflow counters alternate between calls: the fallback
 // launch of call k resets the counter that call k+1 appends to.
@@ -5107,7 +4959,9 @@ int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   if (n > 256 || mode == SH_MODE_TRIPLETS) return SH_DESIGN_LARGE;
   // twins keep the LDS tile: their 128-dword register column does not stay
   // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
-  if (mode == SH_MODE_TWINS) return (flags & SH_FLAG_DT_TILE) ? SH_DESIGN_DT_TWINS : SH_DESIGN_TWINS;
+  // (a one-wave dense-tile twins kernel with 64-bit keys was built in round 4
+  // and measured 36 % slower than this 4-wave one: profiles/r04_twins_dt.jsonl)
+  if (mode == SH_MODE_TWINS) return SH_DESIGN_TWINS;
   if (flags & SH_FLAG_LDS_TILE) return SH_DESIGN_LDS_TILE;
   if (flags & SH_FLAG_DT_TILE) return SH_DESIGN_DT_TILE;
   // (SH_FLAG_SW_TILE, the retired one-wave register-tile kernel, is refused
@@ -5160,7 +5014,6 @@ int resident_blocks(sh_ctx *ctx, int design, int mode, int n, int B) {
       return occ_blocks(ctx, santa_block_kernel<1, 1>, SANTA_WG, santa_lds_layout(n, 1, ctx->ng).total);
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
     case SH_DESIGN_DT_TILE: return dt_tile_slots(ctx, n);
-    case SH_DESIGN_DT_TWINS: return occ_blocks(ctx, santa_dtw_kernel, SANTA_WG, dtw_lds_bytes(n, ctx->ng));
     case SH_DESIGN_VT_TILE: return vt_tile_slots(ctx);
     case SH_DESIGN_SPARSE3:
       return ctx->d_wish10 ? occ_blocks(ctx, santa_sp3_kernel<false, true>, WAVE, 0)
@@ -5203,7 +5056,6 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
       return (flags & SH_FLAG_TIMING) ? launch_santa<1, 0, true>(ctx, a, B, s) : launch_santa<1, 0>(ctx, a, B, s);
     case SH_DESIGN_VT_TILE: return launch_santa_vt_sc(ctx, a, B, s);
     case SH_DESIGN_DT_TILE: return launch_santa_dt(ctx, a, B, s);
-    case SH_DESIGN_DT_TWINS: return launch_santa_dtw(ctx, a, B, s);
     case SH_DESIGN_SPARSE3: return launch_santa_sp(ctx, a, B, s, true);
     default: return launch_santa_sp(ctx, a, B, s, false);
   }

@@ -31,7 +31,7 @@ SH_FLAG_SP1 = 256
 SH_FLAG_TEST_RANGE = 512  # test hook: every register-tile block goes to the fallback launch
 SH_FLAG_NO_APPLY = 1024  # solve without writing the gift types (overlapping blocks allowed)
 SH_FLAG_SP2 = 2048  # retired (round 4): the C-ABI refuses it (SH_ERR_ARGS)
-SH_FLAG_DT_TILE = 4096  # force the dense-tile one-wave kernels (santa_dt_kernel, twins santa_dtw_kernel)
+SH_FLAG_DT_TILE = 4096  # force the dense-tile one-wave kernel (santa_dt_kernel)
 SH_ERRF_ROWS = 1
 SH_ERRF_INFEASIBLE = 2
 SH_ERRF_TYPE = 4
@@ -44,15 +44,13 @@ SH_DESIGN_LARGE = 5
 SH_DESIGN_SPARSE2 = 6
 SH_DESIGN_SPARSE3 = 7
 SH_DESIGN_DT_TILE = 8
-SH_DESIGN_DT_TWINS = 9
 SH_DESIGN_NAMES = {0: "santa_sp_kernel (1-wave sparse LDS tile)", 1: "santa_block_kernel (4-wave LDS byte tile)",
                    2: "(retired: santa_sw_kernel)", 3: "santa_vt_kernel (4-wave register tile)",
                    4: "santa_block_kernel (twins, 4-wave code-pair tile)",
                    5: "santa_big_kernel (row rebuilt from the wishlist)",
                    6: "(retired: santa_sp2_kernel)",
                    7: "santa_sp3_kernel (1-wave sparse register tile built in-kernel, 32-bit lattice keys)",
-                   8: "santa_dt_kernel (LDS byte tile built by 4 waves, solved by 1 wave, 32-bit lattice keys)",
-                   9: "santa_dtw_kernel (twins, LDS code-pair tile built by 4 waves, solved by 1 wave)"}
+                   8: "santa_dt_kernel (LDS byte tile built by 4 waves, solved by 1 wave, 32-bit lattice keys)"}
 SH_MAX_N = 1024
 SH_MAX_N_SANTA = 4096
 

@@ -24,7 +24,7 @@ LIB = os.path.join(ROOT, "mpi-hungarian-method_amd", "santa_hip", "libsanta_hip.
 # held to it)
 NO_SCRATCH = (
     "santa_tile_kernelILi1E",
-    "santa_sp3_kernelILb0ELb0E", "santa_sp3_kernelILb0ELb1E", "santa_dt_kernel", "santa_dtw_kernel", "santa_vt_kernelILi0ELi1E", "santa_vt_kernelILi0ELi0E",
+    "santa_sp3_kernelILb0ELb0E", "santa_sp3_kernelILb0ELb1E", "santa_dt_kernel", "santa_vt_kernelILi0ELi1E", "santa_vt_kernelILi0ELi0E",
     "santa_block_kernelILi1ELi0ELb0E", "santa_block_kernelILi1ELi1ELb0E",
     "santa_big_kernel", "score_kernel", "lsap_i64_kernel", "lsap_f64_kernel",
 )
