@@ -42,7 +42,7 @@ def by_short(agg, main=None):
 
 
 def short(name):
-    for key in ("santa_sp3_kernel", "santa_sp2_kernel", "santa_tile_kernel", "santa_sp_kernel", "santa_vt_kernel", "santa_sw_kernel", "santa_block_kernel",
+    for key in ("santa_sp3_kernel", "santa_dt_kernel", "santa_sp2_kernel", "santa_tile_kernel", "santa_sp_kernel", "santa_vt_kernel", "santa_sw_kernel", "santa_block_kernel",
                 "santa_big_kernel", "score_kernel",
                 "sample_kernel", "lsap_i64_kernel", "lsap_f64_kernel"):
         if key in name:
@@ -79,7 +79,9 @@ def main(src, tag, root):
         w, k = b["warmup"], b["steps"]
         kn = b["roofline"]["kernel"].split(" ")[0].split("<")[0]
         # the register-tile sparse design runs two kernels per solve launch
+        # (one since round 4 with the packed wishlists: the tile is built in-kernel)
         kns = ["santa_tile_kernel", kn] if kn in ("santa_sp2_kernel", "santa_sp3_kernel") else [kn]
+        kns = [x for x in kns if x in trace]
         vs = [trace.get(x, []) for x in kns]
         if all(len(v) >= w + k for v in vs):
             t = [sum(v[i] for v in vs) for i in range(w, w + k)]
