@@ -3377,6 +3377,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
       }
       int nrem = n;
+      uint32_t rq = lds_addr(rem) + 4u * (uint32_t)(n - 1);  // &rem[nrem - 1], stepped down
       int32_t minVal = 0;
       int i = cur;
       int sink;
@@ -3393,14 +3394,16 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         stamp(first ? tD : tC);
         first = false;
         const uint32_t tw = tile2_get(T0, T1, i >> 2);
-        const uint32_t e = (tw >> ((i & 1) << 4)) & 0xFFFFu;
+        // the entry's fields straight from the dword: a bit-field offset uses
+        // bits 4:0 only, so i << 4 selects the 16-bit half (i & 1)
+        const uint32_t sh = (uint32_t)i << 4;
         // the row's half of the wave (lanes 32L.., L = (i >> 1) & 1) as an SGPR mask
         const uint32_t hl = (uint32_t)(-((i >> 1) & 1));
         const bool mine = __builtin_amdgcn_inverse_ballot_w64(((uint64_t)hl << 32) | ~hl);
-        const uint32_t ea = e >> 9;
+        const uint32_t ea = __builtin_amdgcn_ubfe(tw, sh + 9u, 7);
         // expand the row: hit columns get -a (key units), the rest hold a
         // miss; read this lane's four columns; put the misses back (in-order LDS)
-        const int sslot = mine ? (int)(e & 0x1FFu) : 256 + x31;
+        const int sslot = mine ? (int)__builtin_amdgcn_ubfe(tw, sh, 9) : 256 + x31;
         const int32_t sval = -(int32_t)(ea << (9 + SP3_SH));
         if constexpr (TIMED) {  // (A1: the tile fetch and the entry's fields)
           asm volatile("" ::"v"(sslot), "v"(sval));
@@ -3422,7 +3425,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         // per lone step than the same stores by one lane under an exec mask:
         // profiles/r04_ab_stores.jsonl.)
         const uint32_t ua = ubase + 4u * (uint32_t)i;
-        const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
+        const uint32_t ra = rq;
         const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
         const int32_t miss = SP3_MISS;
         uint64_t sv;
@@ -3510,6 +3513,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         kmv = mv & 3;
         rem[pstar] = (uint32_t)mover_v;  // (every lane, same word; a no-op when pstar == last)
         --nrem;
+        rq -= 4u;
         // (branch-free: both the winner's column and its row are formed; the
         // row is the next step's when assigned, the column is the sink if not)
         sink = 4 * lw + kw;

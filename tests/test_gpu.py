@@ -1056,3 +1056,26 @@ def test_small_wishlists_match_oracle(sh, nw, ng, nq):
         assert np.array_equal(types.cpu().numpy(), want_types), (nw, ng, fl)
     assert c.error_flags() == 0
     c.close()
+
+
+@pytest.mark.parametrize("mode,fl", [(0, 4096), (0, 0), (1, 0)])
+def test_dense_tile_build_declines_to_the_chains(sh, ctx, full_data, mode, fl):
+    """Every child on one gift type: a block's 256 columns share that type,
+    more than the packed build's type table holds (255), so the dense-tile
+    kernel (mode 0, SH_FLAG_DT_TILE and the few-block default) and the 4-wave
+    twins kernel decline their fast build and use the type -> column chains;
+    the round equals the oracle's all the same."""
+    n, B = 256, 6
+    rows = ctx.sample_blocks(mode, n, B, 9, 0)
+    t0 = np.zeros_like(full_data.types)
+    t_host = t0.copy()
+    ocol, ocost = oracle.round_blocks(mode, full_data.wish, t_host, rows.cpu().numpy().reshape(B, n),
+                                      ng=full_data.ng)
+    types = torch.from_numpy(t0).cuda()  # (one type everywhere: legal per block, not a real state)
+    col = torch.empty(B * n, dtype=torch.int32, device="cuda")
+    cost = torch.empty(B, dtype=torch.int64, device="cuda")
+    ctx.solve_blocks(mode, rows, n, types, col=col, cost=cost, flags=fl)
+    assert np.array_equal(col.cpu().numpy().reshape(B, n), ocol)
+    assert np.array_equal(cost.cpu().numpy(), ocost)
+    assert np.array_equal(types.cpu().numpy(), t_host)
+    assert ctx.error_flags() == 0
