@@ -3324,20 +3324,22 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   u32x4 lo;            // (one VGPR tuple: a step's book-keeping writes lo[k] by an indexed move)
   uint32_t c4r = ~0u;  // column of row 4*lane + k in byte k
   uint32_t r4c = 0;    // row of column 4*lane + k in byte k (valid where assigned)
-  uint64_t AM[4];      // assigned columns (wave masks, SGPRs; a column, once assigned, stays so)
   // the tie bits of column j = 4 lane + k at a Dijkstra's start (pos = n-1-j):
-  // (asg ? 256 | pos : 255 - pos) << 2 | k = P ^ (asg ? 0x400 : 0x3FC) with
-  // P = pos << 2 | k (255 - pos = pos ^ 255); a column j >= n (never
-  // assigned) has P = ~0x3FC, i.e. lo = ~0
-  uint32_t P[4];
+  // (assigned ? 256 | pos : 255 - pos) << 2 | k, i.e. P ^ 0x400 or P ^ 0x3FC
+  // with P = pos << 2 | k (255 - pos = pos ^ 255), kept as a table LI that
+  // flips by 0x7FC for the one column a Dijkstra assigns (its sink; a column,
+  // once assigned, stays so); a column j >= n (never assigned) holds ~0
+  u32x4 LI;  // (one VGPR tuple: the sink's flip is an indexed move)
+  // `remaining` at a Dijkstra's start: rem[p] = n - 1 - p for this lane's p
+  uint4 rem0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     W[k] = 0;
     Wp[k] = 0;
-    AM[k] = 0;
     const int j = 4 * lane + k;
-    P[k] = j < n ? ((uint32_t)(n - 1 - j) << 2) | (uint32_t)k : ~0x3FCu;
+    LI[k] = j < n ? (((uint32_t)(n - 1 - j) << 2) | (uint32_t)k) ^ 0x3FCu : ~0u;
   }
+  rem0 = make_uint4(n - 1 - 4 * lane, n - 2 - 4 * lane, n - 3 - 4 * lane, n - 4 - 4 * lane);
   // rem[p]: the column at position p of scipy's `remaining`; rowq[n - 1 - t]:
   // the LDS address of u_l[i] for the row i of step t (written by the step's
   // LDS group from the address it reads the dual with)
@@ -3366,16 +3368,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       // Dijkstra set-up: remaining = [n-1 .. 0], every column < n live, spc = inf
       int ln = lane;
       asm volatile("" : "+v"(ln));
+      lo = LI;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool asg = __builtin_amdgcn_inverse_ballot_w64(AM[k]);
-        lo[k] = P[k] ^ (asg ? 0x400u : 0x3FCu);
-        sbp[k] = ~0u;
-      }
-      {
-        const int p0 = n - 1 - 4 * ln;
-        *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
-      }
+      for (int k = 0; k < 4; ++k) sbp[k] = ~0u;
+      *(uint4 *)(rem + 4 * ln) = rem0;
       int nrem = n;
       uint32_t rq = lds_addr(rem) + 4u * (uint32_t)(n - 1);  // &rem[nrem - 1], stepped down
       int32_t minVal = 0;
@@ -3540,8 +3536,18 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       }
       if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       // the sink is the one column this Dijkstra assigns
-#pragma unroll
-      for (int k = 0; k < 4; ++k) AM[k] |= ((sink & 3) == k) ? 1ull << (sink >> 2) : 0ull;
+      {  // the sink is the one column this Dijkstra assigns: flip its start tie bits
+        uint64_t sv;
+        asm volatile(
+            "s_mov_b64 %1, exec\n\t"
+            "s_mov_b64 exec, %2\n\t"
+            "s_set_gpr_idx_on %3, gpr_idx(SRC1,DST)\n\t"
+            "v_xor_b32 %4, 0x7fc, %4\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %1"
+            : "+v"(LI), "=&s"(sv)
+            : "s"(1ull << (sink >> 2)), "s"(sink & 3), "v"(LI.x));
+      }
       // augment along the path from the sink back to cur (registers only; at
       // most n hops -- a path that does not reach cur in n hops can only come
       // from values outside the checked range, and the block is left to the
@@ -3729,16 +3735,22 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
   int32_t W[4], Wp[4];
   u32x4 lo;
   uint32_t c4r = ~0u, r4c = 0;
-  uint64_t AM[4];
-  uint32_t P[4];
+  // the tie bits of column j = 4 lane + k at a Dijkstra's start (pos = n-1-j):
+  // (assigned ? 256 | pos : 255 - pos) << 2 | k, i.e. P ^ 0x400 or P ^ 0x3FC
+  // with P = pos << 2 | k (255 - pos = pos ^ 255), kept as a table LI that
+  // flips by 0x7FC for the one column a Dijkstra assigns (its sink; a column,
+  // once assigned, stays so); a column j >= n (never assigned) holds ~0
+  u32x4 LI;  // (one VGPR tuple: the sink's flip is an indexed move)
+  // `remaining` at a Dijkstra's start: rem[p] = n - 1 - p for this lane's p
+  uint4 rem0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     W[k] = 0;
     Wp[k] = 0;
-    AM[k] = 0;
     const int j = 4 * lane + k;
-    P[k] = j < n ? ((uint32_t)(n - 1 - j) << 2) | (uint32_t)k : ~0x3FCu;
+    LI[k] = j < n ? (((uint32_t)(n - 1 - j) << 2) | (uint32_t)k) ^ 0x3FCu : ~0u;
   }
+  rem0 = make_uint4(n - 1 - 4 * lane, n - 2 - 4 * lane, n - 3 - 4 * lane, n - 4 - 4 * lane);
   uint32_t *rowq = rem + 256;
   const uint32_t ubase = lds_addr(u_l);
   const uint32_t tbase = lds_addr(tile8) + 4u * (uint32_t)lane;
@@ -3754,16 +3766,10 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       if (cur == n - SP3_PRIO_C) __builtin_amdgcn_s_setprio(0);
       int ln = lane;
       asm volatile("" : "+v"(ln));
+      lo = LI;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool asg = __builtin_amdgcn_inverse_ballot_w64(AM[k]);
-        lo[k] = P[k] ^ (asg ? 0x400u : 0x3FCu);
-        sbp[k] = ~0u;
-      }
-      {
-        const int p0 = n - 1 - 4 * ln;
-        *(uint4 *)(rem + 4 * lane) = make_uint4(p0, p0 - 1, p0 - 2, p0 - 3);
-      }
+      for (int k = 0; k < 4; ++k) sbp[k] = ~0u;
+      *(uint4 *)(rem + 4 * ln) = rem0;
       if (lane == 0) rowq[n - 1] = ubase + 4u * (uint32_t)cur;  // (step 0's row)
       int nrem = n;
       int32_t minVal = 0;
@@ -3861,8 +3867,18 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
       }
       if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) AM[k] |= ((sink & 3) == k) ? 1ull << (sink >> 2) : 0ull;
+      {  // the sink is the one column this Dijkstra assigns: flip its start tie bits
+        uint64_t sv;
+        asm volatile(
+            "s_mov_b64 %1, exec\n\t"
+            "s_mov_b64 exec, %2\n\t"
+            "s_set_gpr_idx_on %3, gpr_idx(SRC1,DST)\n\t"
+            "v_xor_b32 %4, 0x7fc, %4\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %1"
+            : "+v"(LI), "=&s"(sv)
+            : "s"(1ull << (sink >> 2)), "s"(sink & 3), "v"(LI.x));
+      }
       int j = sink, pi = -1;
       for (int hop = 0; hop <= n; ++hop) {
         const int jl = j >> 2;
