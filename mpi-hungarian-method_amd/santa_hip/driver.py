@@ -186,10 +186,15 @@ class _Sums:
         d.zero_()
         return d
 
-    def reduce(self, d) -> None:
+    def reduce(self, d):
+        """Start the all-reduce(sum) of d; returns its work handle (None on one
+        rank).  The round's stream does not wait for it: the engine's
+        delta_begin(after=work) makes the reader of d (the side stream) wait,
+        so the 16-byte collective overlaps the next round's solve."""
         if self.world.distributed:
             import torch.distributed as dist
-            dist.all_reduce(d, group=self.world.group)
+            return dist.all_reduce(d, group=self.world.group, async_op=True)
+        return None
 
     @staticmethod
     def combine(base, rnd, dc, dg, full):
@@ -292,9 +297,8 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
         if check_disjoint:
             check_engine_errors(engine, world, types.device)
         if sums.delta:
-            sums.reduce(d)
             sc, sg, bad_tri, bad_tw = sums.combine(
-                cur, rnd, *engine.delta_begin(types, d, sums.check_round(rnd)).result())
+                cur, rnd, *engine.delta_begin(types, d, sums.check_round(rnd), after=sums.reduce(d)).result())
         else:
             sc, sg, bad_tri, bad_tw = engine.score_sums(types)
         if bad_tri or bad_tw:
@@ -358,8 +362,7 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
         if check_disjoint:
             check_engine_errors(engine, world, types.device)
         if sums.delta:
-            sums.reduce(d)
-            return engine.delta_begin(types, d, sums.check_round(r))
+            return engine.delta_begin(types, d, sums.check_round(r), after=sums.reduce(d))
         return engine.score_begin(types)
 
     while True:
@@ -421,18 +424,24 @@ def assert_disjoint(rows: torch.Tensor, mode: int) -> None:
         raise AssertionError("blocks of a round are not disjoint (the in-place apply needs a partition)")
 
 
+def _wait(stream, ev) -> None:
+    """stream waits for ev, unless ev has completed already (then a wait
+    would only add a barrier packet between two block kernels)."""
+    if not ev.query():
+        stream.wait_event(ev)
+
+
 class GPUEngine:
     """Adapter of SantaGPU to the run_rounds engine protocol.
 
-    Two pieces of a round's bookkeeping run on a side stream, off the round's
-    critical path (round 4; each was a launch of its own between two rounds'
-    block kernels: profiles/r03e_kernel_stats.csv):
-      * sampling: round r + 1's blocks depend only on (seed, round r + 1)
-        (A1), so they are sampled while round r solves, into the other of two
-        buffers, after everything that still reads that buffer (round r - 1)
-        was enqueued (sample_kernel, ~10 us per round);
-      * the delta sums' zeroing: a buffer is zeroed right after its host copy
-        was enqueued, ready for its next round (a 16-byte fill, ~4 us)."""
+    After the round's snapshot, the round's bookkeeping runs on a side
+    stream, off the round's critical path: the delta sums' host copy (16
+    bytes, after their all-reduce on N > 1 ranks), the rescore of check
+    rounds, and the delta buffer's zeroing for its next round (a 16-byte
+    fill).  The round's stream carries the sampling, the block kernels and
+    the snapshot copy.  Sampling ahead on the side stream is available
+    (PREFETCH, a ring of buffers: round r's blocks depend only on (seed,
+    round r), A1) but measured slower (profiles/r04_gap_probe.json)."""
 
     def __init__(self, ctx):
         self.ctx = ctx
@@ -447,38 +456,53 @@ class GPUEngine:
             self._side = torch.cuda.Stream(self.ctx.device)
         return self._side
 
+    # rounds sampled ahead on the side stream (ring of PREFETCH + 1 row
+    # buffers); 0 = on the round's stream, the default: a sampling kernel
+    # beside the block kernel runs at its low issue priority for ~550 us and
+    # cost the round 6-19 us more than the same kernel (~10 us) in line
+    # (profiles/r04_gap_probe.json: loop_p0_* against loop_p2_*)
+    PREFETCH = 0
+    SIDE_STREAM = True  # the round's bookkeeping after the snapshot on the side stream
+
     def sample_blocks(self, mode, n, B, seed, rnd):
-        """Round rnd's block rows (A1), prefetched while round rnd - 1 solved
-        when the rounds come in order; round rnd + 1's are started on the side
-        stream.  The returned buffer stays valid until round rnd + 2 is asked
-        for (run_rounds uses it within its round)."""
+        """Round rnd's block rows (A1): sampled on the round's stream, or with
+        PREFETCH = K > 0 taken from the side stream, where rounds rnd + 1 ..
+        rnd + K are started (when the rounds come in order, round rnd was
+        sampled while round rnd - K solved).  The returned buffer stays valid
+        until round rnd + K + 1 is asked for (run_rounds uses it within its
+        round)."""
         dev = self.ctx.device
         key = (mode, n, B, seed)
+        ring = self.PREFETCH + 1
         if self._pf_key != key:
             self._pf_key = key
-            self._pf_buf = [torch.empty(B * n, dtype=torch.int32, device=dev) for _ in range(2)]
-            self._pf_rnd = [None, None]
-            self._pf_ev = [None, None]
+            self._pf_buf = [torch.empty(B * n, dtype=torch.int32, device=dev) for _ in range(ring)]
+            self._pf_rnd = [None] * ring
+            self._pf_ev = [None] * ring
         main = torch.cuda.current_stream(dev)
-        k = rnd & 1
+        k = rnd % ring
         if self._pf_ev[k] is not None:  # (a prefetch into buffer k: wait for it)
-            main.wait_event(self._pf_ev[k])
+            _wait(main, self._pf_ev[k])
             self._pf_ev[k] = None
         if self._pf_rnd[k] != rnd:
             self.ctx.sample_blocks(mode, n, B, seed, rnd, out=self._pf_buf[k])
             self._pf_rnd[k] = rnd
-        j = k ^ 1
-        if self._pf_rnd[j] != rnd + 1:
-            free = torch.cuda.Event()
-            free.record(main)  # (round rnd - 1, the last reader of buffer j, is enqueued)
+        free = None
+        for j in range(rnd + 1, rnd + ring):
+            s = j % ring
+            if self._pf_rnd[s] == j:
+                continue
+            if free is None:
+                free = torch.cuda.Event()
+                free.record(main)  # (rounds <= rnd - 1, the last readers of buffer s, are enqueued)
             side = self._side_stream()
             with torch.cuda.stream(side):
                 side.wait_event(free)
-                self.ctx.sample_blocks(mode, n, B, seed, rnd + 1, out=self._pf_buf[j])
+                self.ctx.sample_blocks(mode, n, B, seed, j, out=self._pf_buf[s])
                 ev = torch.cuda.Event()
                 ev.record(side)
-            self._pf_rnd[j] = rnd + 1
-            self._pf_ev[j] = ev
+            self._pf_rnd[s] = j
+            self._pf_ev[s] = ev
         return self._pf_buf[k]
 
     def zeroed_delta(self, d):
@@ -488,7 +512,7 @@ class GPUEngine:
         if ev is None:
             d.zero_()
         else:
-            torch.cuda.current_stream(d.device).wait_event(ev)
+            _wait(torch.cuda.current_stream(d.device), ev)
         return d
 
     def solve_blocks(self, mode, rows, n, types, delta=None):
@@ -515,13 +539,14 @@ class GPUEngine:
         snapshot back (pipelined rounds)."""
         return self._begin(types, None, True)
 
-    def delta_begin(self, types, d, full: bool):
-        """Delta rounds: snapshot `types`, copy the (all-reduced) delta d to
-        the host and, if `full`, rescore the snapshot on the side stream;
-        result() -> (dS_child, dS_gift, full sums or None)."""
-        return self._begin(types, d, full)
+    def delta_begin(self, types, d, full: bool, after=None):
+        """Delta rounds: snapshot `types`, copy the delta d to the host (once
+        `after`, its all-reduce's work handle, is done) and, if `full`, rescore
+        the snapshot on the side stream; result() -> (dS_child, dS_gift, full
+        sums or None)."""
+        return self._begin(types, d, full, after)
 
-    def _begin(self, types, d, full: bool):
+    def _begin(self, types, d, full: bool, after=None):
         if not hasattr(self, "_snaps"):
             dev = types.device
             self._side_stream()
@@ -535,37 +560,39 @@ class GPUEngine:
         self._k ^= 1
         main = torch.cuda.current_stream(types.device)
         if self._done[k] is not None:
-            main.wait_event(self._done[k])  # the score two rounds back has read the snapshot
+            _wait(main, self._done[k])  # the score two rounds back has read the snapshot
         snap = self._snaps[k]
         snap.copy_(types)
         dhost = self._dhost[k]
-        if d is not None:
-            dhost.copy_(d, non_blocking=True)
-        ready = torch.cuda.Event()
-        ready.record(main)
-        done = ready
-        side = self._side
-        if full:
-            with torch.cuda.stream(side):
+        side = self._side if self.SIDE_STREAM else main
+        # everything after the snapshot runs on the side stream: the delta's
+        # host copy and zeroing, the rescore (round 4: the host copy had been
+        # on the round's stream, one more launch between two block kernels)
+        with torch.cuda.stream(side):
+            if side is not main:
+                ready = torch.cuda.Event()
+                ready.record(main)
                 side.wait_event(ready)
+            if after is not None:
+                after.wait()  # (the side stream waits for the all-reduce of d)
+            if d is not None:
+                dhost.copy_(d, non_blocking=True)
+            if full:
                 self.ctx.score_sums_async(snap, out=self._sums[k])
                 self._host[k].copy_(self._sums[k], non_blocking=True)
-                done = torch.cuda.Event()
-                done.record(side)
-        if d is not None:  # zero d for its next round once its host copy is enqueued
-            with torch.cuda.stream(side):
-                side.wait_event(ready)
+            done = torch.cuda.Event()
+            done.record(side)
+            if d is not None:  # zeroed for its next round (zeroed_delta)
                 d.zero_()
-                z = torch.cuda.Event()
-                z.record(side)
-            self._zero_ev[d.data_ptr()] = z
+                if side is not main:
+                    z = torch.cuda.Event()
+                    z.record(side)
+                    self._zero_ev[d.data_ptr()] = z
         self._done[k] = done
         host = self._host[k]
 
         class _Handle:
             def result(_):
-                if d is not None:
-                    ready.synchronize()
                 done.synchronize()
                 sums = tuple(int(x) for x in host.tolist()) if full else None
                 if d is None:

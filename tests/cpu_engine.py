@@ -54,8 +54,10 @@ class CPUOracleEngine:
     def new_delta(self):
         return torch.zeros(2, dtype=torch.int64)
 
-    def delta_begin(self, types, d, full):
+    def delta_begin(self, types, d, full, after=None):
         """Delta-round protocol (GPUEngine.delta_begin)."""
+        if after is not None:
+            after.wait()  # (d's all-reduce)
         snap = types.clone()
         eng = self
         dv = (int(d[0]), int(d[1]))
