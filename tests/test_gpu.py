@@ -739,13 +739,14 @@ def test_design_dispatch(sh, ctx):
 
 # --------------------------------------------------------------------------- RCCL exchange
 def test_exchange_over_rccl(sh, ctx, full_data):
-    """The per-round exchange (pack -> all-gather -> unpack) through a real
-    RCCL process group (one rank: this box has one GPU; the N>1 logic is
-    covered by the gloo tests).  Catches dtypes RCCL does not carry."""
+    """The per-round exchange (pack -> all-gather -> unpack) and the N>1
+    round loop through a real RCCL process group (one rank: this box has one
+    GPU; the N>1 logic is covered by the gloo tests).  Catches dtypes RCCL
+    does not carry and stream-ordering faults of the async delta all-reduce."""
     import socket
 
     import torch.distributed as dist
-    from santa_hip.driver import GPUEngine, World, exchange
+    from santa_hip.driver import GPUEngine, World, exchange, run_rounds
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -765,6 +766,23 @@ def test_exchange_over_rccl(sh, ctx, full_data):
             # the all-gathered bytes are this rank's packed new types
             assert torch.equal(bufs["recv"][:rows.numel()], want[rows.long()]), mode
             assert torch.equal(types, want), mode
+
+        # the whole N > 1 round loop over this RCCL group: exchange, the delta
+        # all-reduce issued async and waited by the side stream, the error-flag
+        # agreement; same history and state as the one-rank loop
+        class RcclWorld(World):
+            @property
+            def distributed(self) -> bool:
+                return True
+
+        out = []
+        for w in (World(), RcclWorld(0, 1, None)):
+            types = ctx.upload_types(full_data.types)
+            res = run_rounds(GPUEngine(ctx), types, mode=0, n=256, seed=3, max_rounds=5, patience=1 << 30,
+                             world=w, pipeline=True, score_check_every=2)
+            torch.cuda.synchronize()
+            out.append((types.cpu().numpy(), [(st.s_child, st.s_gift, st.score) for st in res.history]))
+        assert np.array_equal(out[0][0], out[1][0]) and out[0][1] == out[1][1]
     finally:
         dist.destroy_process_group()
 
