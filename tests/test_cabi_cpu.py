@@ -225,7 +225,7 @@ def test_lsap_front_end_routes_wide_integers_to_float64(monkeypatch):
 
 def test_bench_roofline_helpers():
     """bench.py's roofline plumbing on the CPU: the register-tile design's
-    launch is two kernels (tile build + solve), and the stored HBM traffic
+    launch has up to two kernels (tile build + solve), and the stored HBM traffic
     comes only from a committed rocprofv3 summary of the same kernel source
     and launch size (otherwise null with a note naming the source hash); one
     kernel name that serves two launch sizes (the 4-wave kernel: the twins
@@ -258,4 +258,7 @@ def test_bench_roofline_helpers():
         hb = s["hbm_bytes_per_launch"]
         est = sum(hb[k]["FETCH_SIZE_bytes"] * f for k, f in zip(raw["kernels"], raw["fetch_correction"]))
         assert t["traffic"] == round(est + raw["WRITE_SIZE"])
-        assert raw["kernels"] == ["santa_tile_kernel", "santa_sp3_kernel"]
+        # (the fused build of round 4: the summary holds santa_sp3_kernel alone;
+        # santa_tile_kernel runs only for contexts without the packed wishlists)
+        assert "santa_sp3_kernel" in raw["kernels"]
+        assert set(raw["kernels"]) <= {"santa_tile_kernel", "santa_sp3_kernel"}
