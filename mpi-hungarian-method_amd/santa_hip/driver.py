@@ -61,19 +61,20 @@ def shard_range(B: int, rank: int, size: int) -> tuple[int, int, int]:
     return b0, b1, per
 
 
-def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = False):
     """Rank-ordered concatenation of every rank's `inp` into `out` (RCCL
     all-gather over xGMI on GPUs).  An all-gather only moves bytes, and
     neither torch's NCCL/RCCL process group nor gloo maps int16, so int16
-    buffers travel as their uint8 bytes (no copy, same HBM bytes)."""
+    buffers travel as their uint8 bytes (no copy, same HBM bytes).
+    async_op: return the work handle (wait() before reading `out`)."""
     import torch.distributed as dist
     if inp.dtype == torch.int16:
         inp, out = inp.contiguous().view(torch.uint8), out.view(torch.uint8)
     try:
-        dist.all_gather_into_tensor(out, inp, group=group)
+        return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
     except (RuntimeError, AttributeError, NotImplementedError):
         parts = list(out.chunk(dist.get_world_size(group)))
-        dist.all_gather(parts, inp, group=group)
+        return dist.all_gather(parts, inp, group=group, async_op=async_op)
 
 
 @dataclass
@@ -98,14 +99,17 @@ class LoopResult:
 
 
 def exchange(engine, world: World, mode: int, rows: torch.Tensor, n: int, B: int,
-             types: torch.Tensor, buffers: dict) -> None:
+             types: torch.Tensor, buffers: dict, during=None) -> None:
     """Make every rank's type vector identical after each solved its shard.
 
     Each rank packs the new types of its own blocks' rows (first twin only
     for pairs), one all-gather concatenates the shards in rank order (each
     padded to `per` blocks), and every rank scatters all of them.  Rank r's
     slice starts at r*per*n, which is where its blocks start in `rows`, and
-    only trailing slots are padding, so recv[:B*n] lines up with rows[:B*n]."""
+    only trailing slots are padding, so recv[:B*n] lines up with rows[:B*n].
+    during: work enqueued on the round's stream while the all-gather runs
+    (it must not touch `types`; the round loop samples the next round's
+    blocks there), before the unpack waits for the collective."""
     b0, b1, per = shard_range(B, world.rank, world.size)
     cnt = per * n
     key = (cnt, world.size)
@@ -118,7 +122,12 @@ def exchange(engine, world: World, mode: int, rows: torch.Tensor, n: int, B: int
     mine = rows[b0 * n:b1 * n]
     if mine.numel():
         engine.pack_types(types, mine, send[:mine.numel()])
-    all_gather_flat(recv, send, world.group)
+    if during is None:
+        all_gather_flat(recv, send, world.group)
+    else:
+        work = all_gather_flat(recv, send, world.group, async_op=True)
+        during()
+        work.wait()
     engine.unpack_types(types, rows[:B * n], recv[:B * n], mode)
 
 
@@ -293,7 +302,7 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
         if b1 > b0:
             engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types, delta=d)
         if world.distributed:
-            exchange(engine, world, mode, rows, n, B, types, buffers)
+            exchange(engine, world, mode, rows, n, B, types, buffers, _next_sampler(engine, mode, n, B, seed, rnd))
         if check_disjoint:
             check_engine_errors(engine, world, types.device)
         if sums.delta:
@@ -358,7 +367,7 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
         if b1 > b0:
             engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types, delta=d)
         if world.distributed:
-            exchange(engine, world, mode, rows, n, B, types, buffers)
+            exchange(engine, world, mode, rows, n, B, types, buffers, _next_sampler(engine, mode, n, B, seed, r))
         if check_disjoint:
             check_engine_errors(engine, world, types.device)
         if sums.delta:
@@ -415,6 +424,15 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
     return res
 
 
+def _next_sampler(engine, mode, n, B, seed, rnd):
+    """The exchange's `during` work: round rnd + 1's blocks, sampled while
+    round rnd's all-gather runs (engines with prefetch_blocks)."""
+    pf = getattr(engine, "prefetch_blocks", None)
+    if pf is None:
+        return None
+    return lambda: pf(mode, n, B, seed, rnd + 1)
+
+
 def assert_disjoint(rows: torch.Tensor, mode: int) -> None:
     """Debug check: the round's blocks share no child.  Rows are
     first members c of units (c, .., c + mode): twins pairs, triplets."""
@@ -465,30 +483,17 @@ class GPUEngine:
     SIDE_STREAM = True  # the round's bookkeeping after the snapshot on the side stream
 
     def sample_blocks(self, mode, n, B, seed, rnd):
-        """Round rnd's block rows (A1): sampled on the round's stream, or with
-        PREFETCH = K > 0 taken from the side stream, where rounds rnd + 1 ..
-        rnd + K are started (when the rounds come in order, round rnd was
-        sampled while round rnd - K solved).  The returned buffer stays valid
-        until round rnd + K + 1 is asked for (run_rounds uses it within its
-        round)."""
-        dev = self.ctx.device
-        key = (mode, n, B, seed)
-        ring = self.PREFETCH + 1
-        if self._pf_key != key:
-            self._pf_key = key
-            self._pf_buf = [torch.empty(B * n, dtype=torch.int32, device=dev) for _ in range(ring)]
-            self._pf_rnd = [None] * ring
-            self._pf_ev = [None] * ring
-        main = torch.cuda.current_stream(dev)
-        k = rnd % ring
-        if self._pf_ev[k] is not None:  # (a prefetch into buffer k: wait for it)
-            _wait(main, self._pf_ev[k])
-            self._pf_ev[k] = None
-        if self._pf_rnd[k] != rnd:
-            self.ctx.sample_blocks(mode, n, B, seed, rnd, out=self._pf_buf[k])
-            self._pf_rnd[k] = rnd
+        """Round rnd's block rows (A1): sampled on the round's stream (or
+        already, by prefetch_blocks), or with PREFETCH = K > 0 taken from the
+        side stream, where rounds rnd + 1 .. rnd + K are started (when the
+        rounds come in order, round rnd was sampled while round rnd - K
+        solved).  The returned buffer (one of max(K + 1, 2)) stays valid
+        until round rnd + max(K + 1, 2) is asked for or prefetched (run_rounds
+        uses it within its round)."""
+        ring, main, k = self._ring(mode, n, B, seed, rnd)
+        self._sample_into(mode, n, B, seed, rnd, main, k)
         free = None
-        for j in range(rnd + 1, rnd + ring):
+        for j in range(rnd + 1, rnd + 1 + self.PREFETCH):
             s = j % ring
             if self._pf_rnd[s] == j:
                 continue
@@ -504,6 +509,33 @@ class GPUEngine:
             self._pf_rnd[s] = j
             self._pf_ev[s] = ev
         return self._pf_buf[k]
+
+    def _ring(self, mode, n, B, seed, rnd):
+        key = (mode, n, B, seed)
+        ring = max(self.PREFETCH + 1, 2)
+        if self._pf_key != key:
+            self._pf_key = key
+            self._pf_buf = [torch.empty(B * n, dtype=torch.int32, device=self.ctx.device) for _ in range(ring)]
+            self._pf_rnd = [None] * ring
+            self._pf_ev = [None] * ring
+        return ring, torch.cuda.current_stream(self.ctx.device), rnd % ring
+
+    def _sample_into(self, mode, n, B, seed, rnd, main, k):
+        if self._pf_ev[k] is not None:  # (a side-stream prefetch into buffer k: wait for it)
+            _wait(main, self._pf_ev[k])
+            self._pf_ev[k] = None
+        if self._pf_rnd[k] != rnd:
+            self.ctx.sample_blocks(mode, n, B, seed, rnd, out=self._pf_buf[k])
+            self._pf_rnd[k] = rnd
+
+    def prefetch_blocks(self, mode, n, B, seed, rnd):
+        """Sample round rnd's blocks now, on the round's stream, for the next
+        sample_blocks(rnd): the N > 1 loop calls it while the previous round's
+        all-gather runs (exchange's `during`), so the sampling kernel overlaps
+        the collective.  Buffer rnd % ring was last read by round rnd - ring
+        (<= rnd - 2), enqueued on this stream before."""
+        _, main, k = self._ring(mode, n, B, seed, rnd)
+        self._sample_into(mode, n, B, seed, rnd, main, k)
 
     def zeroed_delta(self, d):
         """d, zeroed: by the side stream after its previous round's host copy

@@ -28,6 +28,7 @@ class CPUOracleEngine:
         self.nq = nq
         self.n_triplets, self.n_twins = family_sizes(self.nc)
         self.score_log = []  # (S_child, S_gift, types sha) of every scored state
+        self.prefetched = []  # rounds passed to prefetch_blocks
 
     def geometry(self, mode, n):
         if mode == _lib.SH_MODE_SINGLE:
@@ -42,6 +43,11 @@ class CPUOracleEngine:
     def sample_blocks(self, mode, n, B, seed, rnd):
         lo, count, stride, _ = self.geometry(mode, n)
         return torch.from_numpy(sample_blocks(seed, rnd, lo, count, stride, n, B).reshape(-1).copy())
+
+    def prefetch_blocks(self, mode, n, B, seed, rnd):
+        """GPUEngine.prefetch_blocks (the exchange's `during` hook): nothing to
+        prefetch on the host; its presence runs the async all-gather path."""
+        self.prefetched.append(rnd)
 
     def solve_blocks(self, mode, rows, n, types, delta=None):
         t = types.numpy()

@@ -101,7 +101,7 @@ def test_all_gather_sends_rccl_dtypes(monkeypatch):
     from santa_hip.driver import all_gather_flat
     seen = []
 
-    def fake(out, inp, group=None):
+    def fake(out, inp, group=None, async_op=False):
         seen.append((out.dtype, inp.dtype))
         out.copy_(inp.repeat(out.numel() // inp.numel()))
 
