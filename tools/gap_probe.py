@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--mode", default="single")
     ap.add_argument("--seed", type=int, default=2017)
     ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--only", default="", help="comma-separated variant names")
     args = ap.parse_args()
     mode = {"single": 0, "twins": 1}[args.mode]
     n, R = 256, args.rounds
@@ -115,7 +116,10 @@ def main():
                 "sync_sample_side": lambda: run("sync", side_sample=True),
                 "sync_sample_main": lambda: run("sync", main_sample=True),
                 "loop_p2_side": lambda: loop(2, True), "loop_p0_main": lambda: loop(0, False),
-                "loop_p0_side": lambda: loop(0, True), "loop_p2_main": lambda: loop(2, False)}
+                "loop_p0_side": lambda: loop(0, True), "loop_p2_main": lambda: loop(2, False),
+                "loop_p1_side": lambda: loop(1, True)}
+    if args.only:
+        variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     for rep in range(args.reps + 1):
         for name, f in variants.items():
             v = round(f(), 4)
