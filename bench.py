@@ -125,13 +125,16 @@ def cpu_info() -> dict:
             "used": min(used, aff)}
 
 
-def b1_baseline(mode: str, n: int, cores: int, seconds: float) -> dict:
+def b1_baseline(mode: str, n: int, cores: int, seconds: float, max_procs: int | None = None) -> dict:
     """B1: the reference's own round loop as written —
     P ranks, Python n^2 cost loop, scipy, pickled gather/bcast, full rescore
     and the 1M-row CSV every round (oracle/ref_semantics.py) — at P = 8 and
-    P = all leased cores.  Runs as a child process before this process
+    P = all leased cores, at most `max_procs` (the blocks of a round: with
+    more ranks than twin blocks the reference raises IndexError,
+    mpi_twins.py:128,132).  Runs as a child process before this process
     touches the GPU."""
-    procs = sorted({min(8, cores), cores})
+    cap = min(cores, max_procs) if max_procs else cores
+    procs = sorted({min(8, cap), cap})
     cmd = [sys.executable, os.path.join(ROOT, "oracle", "ref_semantics.py"), "--mode", mode,
            "--n", str(n), "--procs", ",".join(map(str, procs)), "--seconds", str(seconds)]
     try:
@@ -153,10 +156,13 @@ def cpu_baselines(args, cpu: dict) -> dict:
     (rank 0, or the `--gpus N` launcher before it starts the ranks): B1 (the
     reference's round as written, in a child process), the C port of the path
     on the leased cores and saturated scipy.  Same workload as the GPU line."""
-    b1 = b1_baseline(args.mode, args.n, cpu["used"], args.b1_seconds) if args.mode != "triplets" else None
     from santa_hip import data as D
+    from santa_hip.sampler import family_sizes, twin_geometry
     sd = D.synthetic(args.seed)
     mode = {"single": 0, "twins": 1, "triplets": 2}[args.mode]
+    # (B1 runs on its own synthetic instance of the same shape: same twin count)
+    cap = twin_geometry(*family_sizes(sd.nc), args.n)[2] if mode == 1 else None
+    b1 = b1_baseline(args.mode, args.n, cpu["used"], args.b1_seconds, cap) if args.mode != "triplets" else None
     cb = cpu_baseline(sd, mode, args.n, args.cpu_seconds, cpu["used"])
     cb["cpu_model"] = cpu["model"]
     cb["nproc"] = cpu["nproc"]
