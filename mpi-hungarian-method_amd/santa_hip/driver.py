@@ -474,8 +474,8 @@ class GPUEngine:
             self._side = torch.cuda.Stream(self.ctx.device)
         return self._side
 
-    # rounds sampled ahead on the side stream (ring of PREFETCH + 1 row
-    # buffers); 0 = on the round's stream, the default: a sampling kernel
+    # rounds sampled ahead on the side stream (ring of max(PREFETCH + 1, 2)
+    # row buffers); 0 = on the round's stream, the default: a sampling kernel
     # beside the block kernel runs at its low issue priority for ~550 us and
     # cost the round 6-19 us more than the same kernel (~10 us) in line
     # (profiles/r04_gap_probe.json: loop_p0_* against loop_p2_*)
