@@ -347,17 +347,19 @@ def stored_traffic(knames, blocks: int, n: int = 256, mode: int = 0):
         if s.get("source_sha16") != src or not _same_launch(s, blocks, n, mode):
             continue
         hb = s.get("hbm_bytes_per_launch", {})
-        # the kernels this launch ran (the last named is the design's main kernel)
-        knames = [k for k in knames[:-1] if k in hb] + knames[-1:]
-        es = [hb.get(k, {}) for k in knames]
+        # the kernels this summary saw the launch run (the last named is the
+        # design's main kernel, always required); filtered per summary, so a
+        # summary without the optional build kernel does not drop it from the next
+        names = [k for k in knames[:-1] if k in hb] + knames[-1:]
+        es = [hb.get(k, {}) for k in names]
         if all("FETCH_SIZE_bytes" in e and "WRITE_SIZE_bytes" in e for e in es):
             cal = json.load(open(calib[-1])) if calib else {}
-            ks = [cal.get("kernel_factors", {}).get(kn, cal.get("gather_correction_factor", 1.0)) for kn in knames]
+            ks = [cal.get("kernel_factors", {}).get(kn, cal.get("gather_correction_factor", 1.0)) for kn in names]
             fetch = sum(e["FETCH_SIZE_bytes"] for e in es)
             write = sum(e["WRITE_SIZE_bytes"] for e in es)
             est = sum(e["FETCH_SIZE_bytes"] * k for e, k in zip(es, ks)) + write
             return {"traffic": round(est),
-                    "traffic_raw": {"FETCH_SIZE": fetch, "WRITE_SIZE": write, "kernels": knames,
+                    "traffic_raw": {"FETCH_SIZE": fetch, "WRITE_SIZE": write, "kernels": names,
                                     "fetch_correction": ks,
                                     "calibration": os.path.basename(calib[-1]) if calib else None},
                     "traffic_source": f"{os.path.basename(path)} (kernel source {src})"}

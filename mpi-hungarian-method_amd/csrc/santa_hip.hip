@@ -4822,6 +4822,10 @@ int launch_santa_vt_sc(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
 // left (out of range; every block under the exact-argmin and range test
 // flags).  Counters alternate as in launch_santa_sp.
 int launch_santa_dt(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
+  // the tile holds rank codes (rank + 1) in uint8 with 255 reserved: the same
+  // guard as the default dispatch, here also for the forced SH_FLAG_DT_TILE
+  // (sh_ctx_create caps n_wish at 127 today, well inside it)
+  if (ctx->n_wish > 254) return fail(SH_ERR_ARGS, "dense tile: n_wish > 254 does not fit the uint8 rank codes");
   const size_t lds = dt_lds_layout(a.n, ctx->ng).total;
   if (lds > 160 * 1024) return fail(SH_ERR_ARGS, "dense tile: too many gift types for LDS");
   static thread_local AttrCache attr;

@@ -35,6 +35,18 @@ SH_FLAG_DT_TILE = 4096  # force the dense-tile one-wave kernel (santa_dt_kernel)
 SH_ERRF_ROWS = 1
 SH_ERRF_INFEASIBLE = 2
 SH_ERRF_TYPE = 4
+_ERRF_TEXT = {SH_ERRF_ROWS: "a block's child ids out of [0, nc)",
+              SH_ERRF_INFEASIBLE: "an infeasible solve",
+              SH_ERRF_TYPE: "a block's current gift type out of [0, ng)"}
+
+
+def describe_error_flags(flags: int) -> str:
+    """The SH_ERRF_* bits of sh_ctx_error_flags as text (unknown bits by value)."""
+    parts = [t for b, t in _ERRF_TEXT.items() if flags & b]
+    rest = flags & ~sum(_ERRF_TEXT)
+    if rest:
+        parts.append(f"unknown bits {rest:#x}")
+    return "; ".join(parts) or "none"
 SH_DESIGN_SPARSE = 0
 SH_DESIGN_LDS_TILE = 1
 SH_DESIGN_SW_TILE = 2

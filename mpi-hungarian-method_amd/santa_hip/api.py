@@ -87,7 +87,7 @@ def _solve_one(mode: int, rows: np.ndarray, types_np: np.ndarray) -> np.ndarray:
     s.solve_blocks(mode, rows_t, n, types, col=col)
     flags = s.error_flags()
     if flags:
-        raise ValueError(f"block rows out of range (device flags {flags})")
+        raise ValueError(f"block not solved: {_lib.describe_error_flags(flags)} (device flags {flags:#x})")
     return col.cpu().numpy().astype(np.int64)
 
 

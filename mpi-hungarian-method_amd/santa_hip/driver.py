@@ -155,7 +155,7 @@ def check_engine_errors(engine, world: World | None = None, device=None) -> None
         flags = sum(int(b) << i for i, b in enumerate(bits.tolist()))
     if flags:
         raise RuntimeError(f"sh_solve_blocks skipped blocks (device error flags {flags:#x}: "
-                           "1 = child id out of range, 2 = infeasible, 4 = gift type out of range)")
+                           f"{_lib.describe_error_flags(flags)})")
 
 
 class _Sums:
@@ -290,6 +290,7 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
                              on_round, best, check_disjoint, res, accept, sums, cur)
         check_engine_errors(engine, world, types.device)
         sums.final_check(types, res.sums, res.history)
+        _drain(engine)
         return res
     for rnd in range(max_rounds):
         t0 = time.perf_counter()
@@ -302,7 +303,8 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
         if b1 > b0:
             engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types, delta=d)
         if world.distributed:
-            exchange(engine, world, mode, rows, n, B, types, buffers, _next_sampler(engine, mode, n, B, seed, rnd))
+            exchange(engine, world, mode, rows, n, B, types, buffers,
+                     _next_sampler(engine, mode, n, B, seed, rnd, max_rounds))
         if check_disjoint:
             check_engine_errors(engine, world, types.device)
         if sums.delta:
@@ -337,7 +339,16 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
     res.sums = cur
     check_engine_errors(engine, world, types.device)
     sums.final_check(types, cur, res.history)
+    _drain(engine)
     return res
+
+
+def _drain(engine) -> None:
+    """Engines with side-stream work (GPUEngine.drain) finish it before the
+    loop returns and its delta buffers are released."""
+    d = getattr(engine, "drain", None)
+    if d is not None:
+        d()
 
 
 def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world, on_round, best,
@@ -367,7 +378,8 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
         if b1 > b0:
             engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types, delta=d)
         if world.distributed:
-            exchange(engine, world, mode, rows, n, B, types, buffers, _next_sampler(engine, mode, n, B, seed, r))
+            exchange(engine, world, mode, rows, n, B, types, buffers,
+                     _next_sampler(engine, mode, n, B, seed, r, max_rounds))
         if check_disjoint:
             check_engine_errors(engine, world, types.device)
         if sums.delta:
@@ -424,11 +436,13 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
     return res
 
 
-def _next_sampler(engine, mode, n, B, seed, rnd):
+def _next_sampler(engine, mode, n, B, seed, rnd, max_rounds):
     """The exchange's `during` work: round rnd + 1's blocks, sampled while
-    round rnd's all-gather runs (engines with prefetch_blocks)."""
+    round rnd's all-gather runs (engines with prefetch_blocks).  None after
+    the last round of the budget (no round rnd + 1 will run; a patience stop
+    cannot be known in advance, so that one round's sampling is spent)."""
     pf = getattr(engine, "prefetch_blocks", None)
-    if pf is None:
+    if pf is None or rnd + 1 >= max_rounds:
         return None
     return lambda: pf(mode, n, B, seed, rnd + 1)
 
@@ -565,6 +579,15 @@ class GPUEngine:
     def error_flags(self):
         return self.ctx.error_flags()
 
+    def drain(self):
+        """End of a run: wait for the side stream's last work (the final
+        round's delta copy and zeroing, a dropped speculative round's rescore)
+        and forget the zeroing events, so that nothing of this run is pending
+        on buffers the caller frees or on the next run's first round."""
+        if hasattr(self, "_side"):
+            self._side.synchronize()
+        self._zero_ev.clear()
+
     def score_begin(self, types):
         """Snapshot `types` and score the snapshot on a side stream; returns a
         handle with result() -> score sums and restore(types) -> copy the
@@ -608,6 +631,8 @@ class GPUEngine:
             if after is not None:
                 after.wait()  # (the side stream waits for the all-reduce of d)
             if d is not None:
+                if side is not main:  # (the allocator must not recycle d under the side stream's work)
+                    d.record_stream(side)
                 dhost.copy_(d, non_blocking=True)
             if full:
                 self.ctx.score_sums_async(snap, out=self._sums[k])

@@ -29,6 +29,7 @@ class CPUOracleEngine:
         self.n_triplets, self.n_twins = family_sizes(self.nc)
         self.score_log = []  # (S_child, S_gift, types sha) of every scored state
         self.prefetched = []  # rounds passed to prefetch_blocks
+        self.drained = 0  # run_rounds' end-of-run drain() calls
 
     def geometry(self, mode, n):
         if mode == _lib.SH_MODE_SINGLE:
@@ -48,6 +49,10 @@ class CPUOracleEngine:
         """GPUEngine.prefetch_blocks (the exchange's `during` hook): nothing to
         prefetch on the host; its presence runs the async all-gather path."""
         self.prefetched.append(rnd)
+
+    def drain(self):
+        """GPUEngine.drain: nothing runs asynchronously on the host."""
+        self.drained += 1
 
     def solve_blocks(self, mode, rows, n, types, delta=None):
         t = types.numpy()

@@ -262,3 +262,14 @@ def test_bench_roofline_helpers():
         # santa_tile_kernel runs only for contexts without the packed wishlists)
         assert "santa_sp3_kernel" in raw["kernels"]
         assert set(raw["kernels"]) <= {"santa_tile_kernel", "santa_sp3_kernel"}
+
+
+def test_error_flags_are_described_by_bit():
+    """The device error flags reach the user as what they mean (an infeasible
+    solve or a bad gift type is not reported as 'rows out of range')."""
+    assert _lib.describe_error_flags(0) == "none"
+    assert "child ids" in _lib.describe_error_flags(_lib.SH_ERRF_ROWS)
+    assert _lib.describe_error_flags(_lib.SH_ERRF_INFEASIBLE) == "an infeasible solve"
+    both = _lib.describe_error_flags(_lib.SH_ERRF_TYPE | _lib.SH_ERRF_INFEASIBLE)
+    assert "gift type" in both and "infeasible" in both and "child ids" not in both
+    assert "unknown bits 0x10" in _lib.describe_error_flags(0x10)

@@ -37,7 +37,8 @@ def _run(eng_data, mode, n, bpr, rounds, world=None):
     types = torch.from_numpy(sd.types.copy())
     res = run_rounds(eng, types, mode=mode, n=n, blocks_per_round=bpr, seed=17,
                      max_rounds=rounds, world=world or World(), patience=100)
-    return types.numpy().copy(), [st.score for st in res.history]
+    assert eng.drained == 1  # (the loop drains the engine's side work once, at its end)
+    return types.numpy().copy(), [st.score for st in res.history], list(eng.prefetched)
 
 
 def _worker(rank, size, port, mode, n, bpr, rounds, out):
@@ -51,8 +52,7 @@ def _worker(rank, size, port, mode, n, bpr, rounds, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=size)
     sd = D.synthetic(**SMALL)
-    t, scores = _run(sd, mode, n, bpr, rounds, World(rank, size, None))
-    out[rank] = (t, scores)
+    out[rank] = _run(sd, mode, n, bpr, rounds, World(rank, size, None))
     dist.destroy_process_group()
 
 
@@ -61,15 +61,18 @@ def _worker(rank, size, port, mode, n, bpr, rounds, out):
 def test_multirank_equals_single_rank(size, mode, n, bpr):
     sd = D.synthetic(**SMALL)
     rounds = 3
-    ref_t, ref_scores = _run(sd, mode, n, bpr, rounds)
+    ref_t, ref_scores, _ = _run(sd, mode, n, bpr, rounds)
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(size, port, mode, n, bpr, rounds, out), nprocs=size, join=True)
     for r in range(size):
-        t, scores = out[r]
+        t, scores, pref = out[r]
         assert np.array_equal(t, ref_t), f"rank {r} state differs"
         assert scores == ref_scores
+        # the exchange samples the next round behind the all-gather, but not
+        # after the budget's last round (no round `rounds` runs)
+        assert pref == list(range(1, rounds)), pref
 
 
 def test_shard_range_covers_blocks():

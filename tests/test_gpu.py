@@ -288,8 +288,10 @@ def _oracle_round_threaded(mode, wish, t_host, r, ng, threads=16):
 def test_bench_rounds_vs_oracle(sh, ctx, full_data, mode, pinned, rounds):
     """The rounds bench.py times, pinned to the oracle on the states they
     actually run from: bench seed 2017, full rounds (3730 singles blocks on the
-    default dispatch, santa_tile_kernel + santa_sp3_kernel with 32-bit lattice
-    keys; 78 twins blocks), the reference's loop (run_rounds) with its default
+    default dispatch: the fused santa_sp3_kernel<.., FUSED = true>, which builds
+    its register tile in-kernel from the packed wishlists and solves in 32-bit
+    lattice keys; 78 twins blocks on santa_block_kernel<1, 1>), the
+    reference's loop (run_rounds) with its default
     delta round sums.
       * pinned rounds: ALL blocks' col and exact cost, the whole new type
         vector, the steps and the deltas equal the oracle solving the same
