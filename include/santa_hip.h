@@ -77,6 +77,10 @@ extern "C" {
                                    (santa_dt_kernel: 4 waves build the LDS
                                    byte tile, one wave solves; singles,
                                    n <= 256; identical results)            */
+#define SH_FLAG_BIG_ROWS 8192u  /* singles n > 256: force the row-rebuild
+                                   kernel (santa_big_kernel) instead of the
+                                   staged-row lattice kernel (A/B; identical
+                                   results)                                 */
 #define SH_FLAG_NO_APPLY 1024u  /* solve and report (col, cost, deltas,
                                    steps) but leave the gift types untouched:
                                    blocks may then overlap (batched
@@ -94,6 +98,11 @@ extern "C" {
                                 32-bit lattice keys (full rounds, default)  */
 #define SH_DESIGN_DT_TILE 8  /* byte tile in LDS built by 4 waves, solved by
                                 one wave, 32-bit lattice keys (few blocks)  */
+#define SH_DESIGN_LARGE_LB 9 /* singles 256 < n <= 2048: each wave's
+                                candidate row staged as a per-gift-type cost
+                                table in LDS before the step's argmin,
+                                32-bit lattice keys (santa_lb_kernel; blocks
+                                out of its range: santa_big_kernel)        */
 
 /* Largest block size (rows = columns) the batched solvers accept. */
 #define SH_MAX_N 1024

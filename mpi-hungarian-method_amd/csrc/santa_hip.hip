@@ -4052,11 +4052,79 @@ __device__ __forceinline__ uint32_t wish_code(const SantaArgs &a, int child, int
   return 0u;
 }
 
+// Outputs of a large block (santa_big_kernel, santa_lb_kernel): the matched
+// codes recovered by scanning each child's wishlist for the new and the old
+// gift (exact cost, happiness deltas), col, steps, then the in-place apply.
+// c4r: the solve's col4row; ctype: the columns' (old) gift types; part: NW x 3
+// int64 of LDS scratch.
+template <int MODE, int NW>
+__device__ __forceinline__ void big_block_outputs(const SantaArgs &a, const int b, const int n, const int16_t *c4r,
+                                                  const int16_t *ctype, const int32_t *rows_l, int64_t *part,
+                                                  const int64_t steps, const int fallbacks) {
+  constexpr int WG = NW * WAVE;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nw1 = a.n_wish + 1;
+  int64_t cost = 0, dch = 0, dgh = 0;
+  for (int i = tid; i < n; i += WG) {
+    const int col = c4r[i];
+    const int told = ctype[i], tnew = ctype[col];
+    const int child = rows_l[i];
+    const uint32_t n1 = wish_code(a, child, tnew), o1 = wish_code(a, child, told);
+    if (MODE == 0) {
+      cost += single_cost(n1, nw1, a.E);
+      dch += child_happy(n1, nw1) - child_happy(o1, nw1);
+      if (a.delta) dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
+    } else if (MODE == 2) {
+      const uint32_t n2 = wish_code(a, child + 1, tnew), o2 = wish_code(a, child + 1, told);
+      const uint32_t n3 = wish_code(a, child + 2, tnew), o3 = wish_code(a, child + 2, told);
+      cost += triplet_cost(n1 | (n2 << 8) | (n3 << 16), nw1, a.E);
+      dch += child_happy(n1, nw1) + child_happy(n2, nw1) + child_happy(n3, nw1) -
+             child_happy(o1, nw1) - child_happy(o2, nw1) - child_happy(o3, nw1);
+      if (a.delta)
+        for (int m = 0; m < 3; ++m) dgh += gift_happy(a, child + m, tnew) - gift_happy(a, child + m, told);
+    } else {
+      const uint32_t n2 = wish_code(a, child + 1, tnew), o2 = wish_code(a, child + 1, told);
+      cost += twin_cost(n1 | (n2 << 8), nw1, a.E);
+      dch += child_happy(n1, nw1) + child_happy(n2, nw1) - child_happy(o1, nw1) - child_happy(o2, nw1);
+      if (a.delta) dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
+             gift_happy(a, child, told) - gift_happy(a, child + 1, told);
+    }
+    if (a.col) a.col[(size_t)b * n + i] = col;
+  }
+  cost = wave_sum_i64(cost);
+  dch = wave_sum_i64(dch);
+  dgh = wave_sum_i64(dgh);
+  if (lane == 0) {
+    part[3 * w + 0] = cost;
+    part[3 * w + 1] = dch;
+    part[3 * w + 2] = dgh;
+  }
+  __syncthreads();  // every old type was read from ctype (LDS): apply in place
+  for (int i = tid; i < n; i += WG) {
+    const int16_t tnew = ctype[c4r[i]];
+    if (!(a.flags & SH_FLAG_NO_APPLY)) for (int m = 0; m <= MODE; ++m) a.types[rows_l[i] + m] = tnew;
+  }
+  if (tid == 0) {
+    int64_t tc = 0, t0 = 0, t1 = 0;
+    for (int q = 0; q < NW; ++q) {
+      tc += part[3 * q];
+      t0 += part[3 * q + 1];
+      t1 += part[3 * q + 2];
+    }
+    if (a.cost) a.cost[b] = tc;
+    if (a.steps) a.steps[b] = steps;
+    if (a.delta) {
+      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)t0);
+      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)t1);
+    }
+    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
+  }
+}
+
 template <int MODE, int NW, int K, int FB>
-__global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
+__device__ __forceinline__ void santa_big_block(const SantaArgs &a, const int b) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int WG = NW * WAVE;
-  const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n = a.n;
   const BigLds L = big_lds_layout(n, MODE, a.ng, NW, K);
@@ -4139,60 +4207,394 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
                                                          (a.flags & SH_FLAG_EXACT_ARGMIN) != 0);
   }
   // -- outputs ----------------------------------------------------------------------
-  int64_t cost = 0, dch = 0, dgh = 0;
+  big_block_outputs<MODE, NW>(a, b, n, S.c4r, ctype, rows_l, part, steps, fallbacks);
+}
+
+// One block per workgroup, or (a.blist) the fallback launch of santa_lb_kernel:
+// a workgroup per CU loops over the listed blocks (the lattice kernel left
+// them untouched: out of its checked range, or every block under the test
+// flags) and resets the other parity's list counter for the next call.
+template <int MODE, int NW, int K, int FB>
+__global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
+  if (a.blist) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.ovf_reset) *a.ovf_reset = 0;
+    const int cnt = *a.bcount;
+    for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
+      santa_big_block<MODE, NW, K, FB>(a, a.blist[q]);
+      __syncthreads();  // (LDS reused by the next listed block)
+    }
+  } else {
+    santa_big_block<MODE, NW, K, FB>(a, blockIdx.x);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// santa_lb_kernel: large singles blocks (256 < n <= 2048; the reference's own
+// n = 2000, mpi_single.py:238) in 32-bit lattice units, with every wave's
+// candidate row staged in LDS before the step's cross-wave argmin.
+//
+// santa_big_kernel rebuilds the winning row after each step's argmin: the
+// row's identity is only known after the fold, so every step waits for a
+// dependent wishlist load (L2 misses: the block's 2000 rows are 400 KB),
+// then the type-table and sorted-column lookups, a scatter and a second
+// barrier (~3,100 cycles per lone step).  Here the global winner of a step
+// is always one of the NW wave minima, each known before the fold: every wave
+// stages the row of its own candidate (if that candidate column is assigned
+// and its row is not staged already) into one of two LDS tables of its own,
+// while the fold's ds_min and barrier run.  A table holds the row's cost of
+// every GIFT TYPE (ng int16: a wish -a * 256, a miss 1), so the next step
+// reads each column's cost as tbl[winner's table][type of the column]: one
+// ds_read per column, no scatter, no second barrier.  The wave whose table
+// the step reads writes its next candidate into its other table.
+//
+// Units (exact, checked): V = A * 256 + m for A * 2^32 + m * E (the lattice
+// of santa_sp3_kernel, base 256 so that a wish fits int16; |m| <= 127 keeps
+// the packing exact, 2 * 127 * E < 2^32).  sbp = (spc_V + 2^19) << 12 | t
+// with t the Dijkstra step of the column's last improvement (one v_min keeps
+// scipy's strict <, the path row is rowq[t]); key = sbp & ~0xFFF | tie, tie =
+// class 1 | pkey 11 (scipy's order among equal values: the last unassigned
+// column in `remaining`, else the first).  The step word folded with ds_min_u64
+// is key << 32 | column << 16 | row4col << 5 | table.  Range (the boxes of
+// LatticeRange in base 256): u~ = u - minVal |A| < 1024, |m| <= 2^bU; W = -v
+// |A| < 512, |m| <= 2^cW, 2^cW + 1 + 2^bU <= 127, so every relaxation value
+// has |V| < 2^19; a block that leaves them is left untouched and re-solved by
+// santa_big_kernel (the fallback launch over its list).
+// ---------------------------------------------------------------------------
+constexpr int LB_TSH = 12;                 // sbp's step field and the key's tie field
+constexpr int32_t LB_BIAS = 1 << 19;       // spc_V + BIAS in [0, 2^20)
+constexpr int LB_MAX_N = 2048;             // 11-bit positions
+struct LbLds {
+  size_t u, c4r, r4c, path, rem, rowq, rows, ctype, tbl, words, part, total;
+  int TS;  // table stride (int16 entries)
+};
+__host__ __device__ __forceinline__ LbLds lb_lds_layout(int n, int ng, int nw, int k) {
+  LbLds L;
+  size_t o = 0;
+  L.TS = (ng + 1) & ~1;
+  L.u = o;     o += r16((size_t)n * 4);
+  L.c4r = o;   o += r16((size_t)n * 2);
+  L.r4c = o;   o += r16((size_t)n * 2);
+  L.path = o;  o += r16((size_t)n * 2);
+  L.rem = o;   o += r16((size_t)n * 2);
+  L.rowq = o;  o += r16((size_t)n * 2);
+  L.rows = o;  o += r16((size_t)n * 4);
+  L.ctype = o; o += r16((size_t)nw * 64 * k * 2);
+  L.tbl = o;   o += r16((size_t)(2 * nw + 2) * L.TS * 2);
+  L.words = o; o += 32;
+  L.part = o;  o += r16((size_t)nw * 3 * 8);
+  L.total = o;
+  return L;
+}
+
+// range boxes of santa_lb_kernel (base 256): t = V + C has no bit of MASK set
+// exactly when |A| < 2^(H - 8) and m lies in [1 - 2^b, 2^b]
+struct LbRange {
+  uint32_t CU, MU, CW, MW;
+  bool ok;
+  __host__ __device__ explicit LbRange(int M) {  // M: the largest |m| compared exactly (<= 127)
+    const int m3 = M / 3 > 1 ? M / 3 : 1;
+    const int cw = 31 - __builtin_clz((uint32_t)m3);
+    const int rest = M - 1 - (1 << cw);
+    const int bu = 31 - __builtin_clz((uint32_t)(rest > 1 ? rest : 1));
+    ok = M >= 3 && (1 << cw) + 1 + (1 << bu) <= M;
+    CU = (1u << 18) + (1u << bu) - 1u;
+    MU = 0xFFF80000u | (255u & ~((2u << bu) - 1u));
+    CW = (1u << 17) + (1u << cw) - 1u;
+    MW = 0xFFFC0000u | (255u & ~((2u << cw) - 1u));
+  }
+};
+
+// TIMED (dev, SH_FLAG_TIMING): every wave sums s_memtime cycles per segment of
+// its steps and writes them to col[b * n + 8 w + q]: 0 table reads + relaxation
+// + lane minimum, 1 wave DPP minimum, 2 candidate (readlanes, row staging, the
+// fold), 3 barrier, 4 word read + decode + book-keeping, 5 per-Dijkstra work,
+// 6 the number of rows this wave staged.
+template <int NW, int K, bool TIMED = false>
+__global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int WG = NW * WAVE;
+  constexpr int NCOL = WG * K;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = a.n, nw = a.n_wish;
+  const LbLds L = lb_lds_layout(n, a.ng, NW, K);
+  const int TS = L.TS;
+  int32_t *u32 = (int32_t *)(smem + L.u);
+  int16_t *c4r = (int16_t *)(smem + L.c4r);
+  int16_t *r4c_l = (int16_t *)(smem + L.r4c);
+  int16_t *path_l = (int16_t *)(smem + L.path);
+  int16_t *rem = (int16_t *)(smem + L.rem);
+  int16_t *rowq = (int16_t *)(smem + L.rowq);
+  int32_t *rows_l = (int32_t *)(smem + L.rows);
+  int16_t *ctype = (int16_t *)(smem + L.ctype);
+  int16_t *tbl = (int16_t *)(smem + L.tbl);
+  uint64_t *words = (uint64_t *)(smem + L.words);
+  int64_t *part = (int64_t *)(smem + L.part);
+
+  // -- rows, types, range checks (as santa_big_kernel) ---------------------------------
+  int bad = 0;
+  for (int j = tid; j < n; j += WG) {
+    const int r = a.rows[(size_t)b * n + j];
+    bad |= (r < 0) || (r >= a.nc);
+    rows_l[j] = r;
+  }
+  if (__syncthreads_or(bad)) {
+    if (tid == 0) atomicOr(a.err, SH_ERRF_ROWS);
+    return;
+  }
+  int badt = 0;
+  for (int j = tid; j < NCOL; j += WG) {
+    const int ty = j < n ? a.types[rows_l[j]] : 0;
+    badt |= (ty < 0) || (ty >= a.ng);
+    ctype[j] = (int16_t)ty;
+  }
+  if (__syncthreads_or(badt)) {
+    if (tid == 0) atomicOr(a.err, SH_ERRF_TYPE);
+    return;
+  }
+  {  // every table entry a miss (V = 1)
+    uint32_t *t32 = (uint32_t *)tbl;
+    const int nd = (2 * NW + 2) * TS / 2;
+    for (int q = tid; q < nd; q += WG) t32[q] = 0x00010001u;
+  }
   for (int i = tid; i < n; i += WG) {
-    const int col = S.c4r[i];
-    const int told = ctype[i], tnew = ctype[col];
-    const int child = rows_l[i];
-    const uint32_t n1 = wish_code(a, child, tnew), o1 = wish_code(a, child, told);
-    if (MODE == 0) {
-      cost += single_cost(n1, nw1, a.E);
-      dch += child_happy(n1, nw1) - child_happy(o1, nw1);
-      if (a.delta) dgh += gift_happy(a, child, tnew) - gift_happy(a, child, told);
-    } else if (MODE == 2) {
-      const uint32_t n2 = wish_code(a, child + 1, tnew), o2 = wish_code(a, child + 1, told);
-      const uint32_t n3 = wish_code(a, child + 2, tnew), o3 = wish_code(a, child + 2, told);
-      cost += triplet_cost(n1 | (n2 << 8) | (n3 << 16), nw1, a.E);
-      dch += child_happy(n1, nw1) + child_happy(n2, nw1) + child_happy(n3, nw1) -
-             child_happy(o1, nw1) - child_happy(o2, nw1) - child_happy(o3, nw1);
-      if (a.delta)
-        for (int m = 0; m < 3; ++m) dgh += gift_happy(a, child + m, tnew) - gift_happy(a, child + m, told);
-    } else {
-      const uint32_t n2 = wish_code(a, child + 1, tnew), o2 = wish_code(a, child + 1, told);
-      cost += twin_cost(n1 | (n2 << 8), nw1, a.E);
-      dch += child_happy(n1, nw1) + child_happy(n2, nw1) - child_happy(o1, nw1) - child_happy(o2, nw1);
-      if (a.delta) dgh += gift_happy(a, child, tnew) + gift_happy(a, child + 1, tnew) -
-             gift_happy(a, child, told) - gift_happy(a, child + 1, told);
-    }
-    if (a.col) a.col[(size_t)b * n + i] = col;
+    u32[i] = 0;
+    c4r[i] = -1;
+    r4c_l[i] = -1;
+    rem[i] = (int16_t)(n - 1 - i);
   }
-  cost = wave_sum_i64(cost);
-  dch = wave_sum_i64(dch);
-  dgh = wave_sum_i64(dgh);
-  if (lane == 0) {
-    part[3 * w + 0] = cost;
-    part[3 * w + 1] = dch;
-    part[3 * w + 2] = dgh;
-  }
-  __syncthreads();  // every old type was read from ctype (LDS): apply in place
-  for (int i = tid; i < n; i += WG) {
-    const int16_t tnew = ctype[S.c4r[i]];
-    if (!(a.flags & SH_FLAG_NO_APPLY)) for (int m = 0; m <= MODE; ++m) a.types[rows_l[i] + m] = tnew;
-  }
-  if (tid == 0) {
-    int64_t tc = 0, t0 = 0, t1 = 0;
-    for (int q = 0; q < NW; ++q) {
-      tc += part[3 * q];
-      t0 += part[3 * q + 1];
-      t1 += part[3 * q + 2];
+  if (tid < 3) words[tid] = ~0ull;
+  __syncthreads();
+
+  // the lattice bound: |m| <= M keeps every compared value exact
+  const int Mb = (int)min((int64_t)127, (int64_t)(0xFFFFFFFFll / a.E) / 2);
+  const LbRange R(Mb);
+  bool big = !R.ok || (a.flags & (SH_FLAG_TEST_RANGE | SH_FLAG_EXACT_ARGMIN)) != 0;
+  int64_t steps = 0;
+
+  if (!big && !(a.flags & SH_FLAG_BUILD_ONLY)) {
+    // per-thread columns j = (w * K + k) * 64 + lane
+    int ct[K];                 // the column's gift type (table index)
+    int32_t W[K];              // -v
+    uint32_t sbp[K], lo[K];    // path-step-tagged spc; tie bits (~0: left `remaining`)
+    int rc[K], crow[K];        // row4col, and that row's child id
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      ct[k] = ctype[(w * K + k) * WAVE + lane];
+      W[k] = 0;
     }
-    if (a.cost) a.cost[b] = tc;
-    if (a.steps) a.steps[b] = steps;
-    if (a.delta) {
-      atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)t0);
-      atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)t1);
+    // tables 2w, 2w + 1 of this wave: the children they hold and, per lane,
+    // the two gifts this lane wrote there (g0 | g1 << 16; 0xFFFF none)
+    int chT0 = -1, chT1 = -1, lastSel = 0;
+    uint32_t og0 = ~0u, og1 = ~0u;
+    // row cur's table (2 NW + (cur & 1)), staged by the last wave one
+    // Dijkstra ahead
+    uint32_t ogC0 = ~0u, ogC1 = ~0u;
+    auto stage = [&](int slot, int child, uint32_t &ogs) {
+      int16_t *T = tbl + slot * TS;
+      const int16_t *src = a.wish + (size_t)(uint32_t)child * (uint32_t)nw;
+      const int g0 = lane < nw ? src[lane] : -1;
+      const int g1 = lane + WAVE < nw ? src[lane + WAVE] : -1;
+      const uint32_t o0 = ogs & 0xFFFFu, o1 = ogs >> 16;
+      if (o0 != 0xFFFFu) T[o0] = 1;  // (one wave: its clears land before its writes)
+      if (o1 != 0xFFFFu) T[o1] = 1;
+      if (g0 >= 0) T[g0] = (int16_t)(-(nw - lane) * 256);
+      if (g1 >= 0) T[g1] = (int16_t)(-(nw - lane - WAVE) * 256);
+      ogs = (uint32_t)(g0 & 0xFFFF) | ((uint32_t)(g1 & 0xFFFF) << 16);
+    };
+    if (w == NW - 1) stage(2 * NW, rows_l[0], ogC0);
+    __syncthreads();
+    uint32_t accU = 0, accW = 0;
+    int par = 0;  // rotating step word
+    uint64_t seg[6] = {0, 0, 0, 0, 0, 0}, ts = 0;
+    uint32_t nstaged = 0;
+    auto stamp = [&](int q) {
+      if constexpr (TIMED) {
+        const uint64_t x = __builtin_amdgcn_s_memtime();
+        seg[q] += x - ts;
+        ts = x;
+      }
+    };
+    if constexpr (TIMED) ts = __builtin_amdgcn_s_memtime();
+    for (int cur = 0; cur < n; ++cur) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int j = (w * K + k) * WAVE + lane;
+        const int rr = j < n ? r4c_l[j] : -1;
+        rc[k] = rr;
+        crow[k] = rr >= 0 ? rows_l[rr] : -1;
+        const int p = n - 1 - j;
+        lo[k] = j >= n ? ~0u : rr < 0 ? (uint32_t)(2047 - p) : (2048u | (uint32_t)p);
+        sbp[k] = ~0u;
+      }
+      int nrem = n, t = 0, i = cur, sink = 0;
+      int32_t minVal = 0, ui = 0;
+      int tb = 2 * NW + (cur & 1);
+      stamp(5);
+      for (;;) {
+        ++steps;
+        if (tid == 0) {
+          rowq[t] = (int16_t)i;
+          words[par == 2 ? 0 : par + 1] = ~0ull;  // re-arm the next step's word
+        }
+        int32_t c[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) c[k] = tbl[tb * TS + ct[k]];
+        const int32_t ut = ui - minVal;
+        accU |= (uint32_t)ut + R.CU;
+        const uint32_t bse = (uint32_t)(LB_BIAS - ut);
+        uint32_t best = ~0u;
+        int bk = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const uint32_t r = (uint32_t)W[k] + (uint32_t)c[k] + bse;
+          sbp[k] = min(sbp[k], (r << LB_TSH) | (uint32_t)t);
+          const uint32_t key = (sbp[k] & ~((1u << LB_TSH) - 1u)) | lo[k];
+          const bool lt = key < best;
+          best = lt ? key : best;
+          bk = lt ? k : bk;
+        }
+        if constexpr (TIMED) asm volatile("" ::"v"(best), "v"(bk));
+        stamp(0);
+        const uint32_t wmin = wave_min_u32_dpp(best);
+        if constexpr (TIMED) asm volatile("" ::"s"(wmin));
+        stamp(1);
+        if (wmin != ~0u) {
+          const uint64_t bal = __builtin_amdgcn_ballot_w64(best == wmin);
+          const int wl = (int)__builtin_ctzll(bal);
+          const int kk = __builtin_amdgcn_readlane(bk, wl);
+          int rr = -1, ch = -1;
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+            if (k == kk) {
+              rr = __builtin_amdgcn_readlane(rc[k], wl);
+              ch = __builtin_amdgcn_readlane(crow[k], wl);
+            }
+          const int col = (w * K + kk) * WAVE + wl;
+          int slot = 0;
+          if (rr >= 0) {  // an assigned candidate: its row staged in one of this wave's tables
+            if (ch == chT0) {
+              slot = 2 * w;
+              lastSel = 0;
+            } else if (ch == chT1) {
+              slot = 2 * w + 1;
+              lastSel = 1;
+            } else {
+              int v = lastSel ^ 1;  // the table not used last, unless the step reads it
+              if (2 * w + v == tb) v ^= 1;
+              if (v == 0) {
+                stage(2 * w, ch, og0);
+                chT0 = ch;
+              } else {
+                stage(2 * w + 1, ch, og1);
+                chT1 = ch;
+              }
+              ++nstaged;
+              slot = 2 * w + v;
+              lastSel = v;
+            }
+          }
+          const uint64_t word = ((uint64_t)wmin << 32) | ((uint32_t)col << 16) |
+                                ((uint32_t)(rr & 0x7FF) << 5) | (uint32_t)slot;
+          if (lane == 0)
+            __hip_atomic_fetch_min(words + par, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        // row cur + 1, staged during Dijkstra cur's first step
+        if (t == 0 && w == NW - 1 && cur + 1 < n) {
+          if ((cur + 1) & 1) stage(2 * NW + 1, rows_l[cur + 1], ogC1);
+          else stage(2 * NW, rows_l[cur + 1], ogC0);
+        }
+        if constexpr (TIMED) __builtin_amdgcn_s_waitcnt(0);
+        stamp(2);
+        __syncthreads();
+        stamp(3);
+        const uint64_t g = words[par];
+        const int last = nrem - 1;
+        const int mcol = rem[last];
+        par = par == 2 ? 0 : par + 1;
+        const uint32_t gk = (uint32_t)(g >> 32), gl = (uint32_t)g;
+        if (gk == ~0u) {  // no live column left without a sink: only from values out of range
+          big = true;
+          break;
+        }
+        minVal = (int32_t)(gk >> LB_TSH) - LB_BIAS;
+        const bool assigned = (gk >> 11) & 1u;
+        const int pk = (int)(gk & 2047u);
+        const int pstar = assigned ? pk : 2047 - pk;
+        const int gcol = (int)(gl >> 16);
+        // book-keeping: the winner leaves `remaining`, the column at position
+        // `last` takes position pstar (its tie bits flip by last ^ pstar)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int j = (w * K + k) * WAVE + lane;
+          lo[k] = (j == gcol) ? ~0u : (j == mcol && pstar != last) ? (lo[k] ^ (uint32_t)(last ^ pstar)) : lo[k];
+        }
+        if (tid == 0 && pstar != last) rem[pstar] = (int16_t)mcol;
+        nrem = last;
+        ++t;
+        if (!assigned) {
+          sink = gcol;
+          break;
+        }
+        i = (int)((gl >> 5) & 0x7FFu);
+        tb = (int)(gl & 31u);
+        ui = u32[i];
+        if constexpr (TIMED) asm volatile("" ::"s"(ui));
+        stamp(4);
+      }
+      stamp(4);
+      if (big) break;  // (block-uniform: every wave read the same word)
+      // dual update of the visited columns and their rows, path rows
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int j = (w * K + k) * WAVE + lane;
+        if (j < n && lo[k] == ~0u) {
+          const int32_t d = minVal - ((int32_t)(sbp[k] >> LB_TSH) - LB_BIAS);
+          W[k] += d;
+          if (rc[k] >= 0) u32[rc[k]] += d;
+          path_l[j] = rowq[sbp[k] & ((1u << LB_TSH) - 1u)];
+        }
+        if (j < n) accW |= (uint32_t)W[k] + R.CW;
+      }
+      if (tid == 0) u32[cur] += minVal;
+      __syncthreads();
+      if (tid == 0) {  // augment along the path from the sink back to cur (<= n hops)
+        int jj = sink, pi = -1;
+        for (int hop = 0; hop <= n; ++hop) {
+          pi = path_l[jj];
+          r4c_l[jj] = (int16_t)pi;
+          const int tt = c4r[pi];
+          c4r[pi] = (int16_t)jj;
+          jj = tt;
+          if (pi == cur) break;
+        }
+        big |= pi != cur;
+      }
+      for (int p = tid; p < n; p += WG) rem[p] = (int16_t)(n - 1 - p);
+      __syncthreads();
     }
-    if (fallbacks) atomicAdd(a.err + 1, fallbacks);
+    stamp(5);
+    if constexpr (TIMED) {
+      if (lane == 0 && a.col) {
+        int32_t *o = a.col + (size_t)b * n + 8 * w;
+        for (int q = 0; q < 6; ++q) o[q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
+        o[6] = (int32_t)nstaged;
+      }
+    }
+    big |= (accU & R.MU) != 0 || (accW & R.MW) != 0;
+  } else if (!big) {
+    for (int i = tid; i < n; i += WG) c4r[i] = (int16_t)i;
+  }
+  if (__syncthreads_or(big)) {  // left untouched: solved by the fallback launch
+    if (tid == 0) a.ovf_list[atomicAdd(a.ovf_cnt, 1)] = b;
+    return;
+  }
+  if constexpr (TIMED) {  // (col holds the segments: outputs without col)
+    SantaArgs a2 = a;
+    a2.col = nullptr;
+    big_block_outputs<0, NW>(a2, b, n, c4r, ctype, rows_l, part, steps, 0);
+  } else {
+    big_block_outputs<0, NW>(a, b, n, c4r, ctype, rows_l, part, steps, 0);
   }
 }
 
@@ -4731,7 +5133,10 @@ int launch_big_cfg(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) 
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total));
     attr.set(ctx->device, L.total);
   }
-  hipLaunchKernelGGL((santa_big_kernel<MODE, NW, K, FB>), dim3(B), dim3(NW * WAVE), L.total, s, a);
+  // (the fallback launch of santa_lb_kernel, a block list: a workgroup per CU
+  // loops over it)
+  const int grid = a.blist ? std::max(1, std::min(B, ctx->n_cu)) : B;
+  hipLaunchKernelGGL((santa_big_kernel<MODE, NW, K, FB>), dim3(grid), dim3(NW * WAVE), L.total, s, a);
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
@@ -4769,14 +5174,6 @@ int with_big_cfg(const sh_ctx *ctx, int n, int B, F &&f) {
   return f(BigCfg<16, 4, 12>{});
 }
 
-template <int MODE>
-int launch_santa_big(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
-  return with_big_cfg<MODE>(ctx, a.n, B, [&](auto c) {
-    using C = decltype(c);
-    return launch_big_cfg<MODE, C::NW, C::K, C::FB>(ctx, a, B, s);
-  });
-}
-
 // The overflow lists of the designs with a fallback launch (block ids, two
 // counters that alternate between calls).
 int ensure_ovf(sh_ctx *ctx, int B, hipStream_t s) {
@@ -4792,6 +5189,86 @@ int ensure_ovf(sh_ctx *ctx, int B, hipStream_t s) {
   }
   return SH_OK;
 }
+
+// santa_lb_kernel's configuration for n (NW * 64 * K >= n columns; the word's
+// table field holds 2 NW + 2 <= 31 tables)
+template <typename F>
+int with_lb_cfg(int n, F &&f) {
+  if (n <= 512) return f(BigCfg<2, 4, 0>{});
+  if (n <= 1024) return f(BigCfg<4, 4, 0>{});
+  return f(BigCfg<8, 4, 0>{});
+}
+
+size_t lb_lds_bytes(const sh_ctx *ctx, int n) {
+  return with_lb_cfg(n, [&](auto c) -> size_t {
+    using C = decltype(c);
+    return lb_lds_layout(n, ctx->ng, C::NW, C::K).total;
+  });
+}
+
+// singles blocks the staged-row lattice kernel takes: 256 < n <= 2048 whose
+// LDS fits (the tables hold ng int16 entries each)
+bool lb_eligible(const sh_ctx *ctx, int n, unsigned flags) {
+  return n > 256 && n <= LB_MAX_N && !(flags & SH_FLAG_BIG_ROWS) && lb_lds_bytes(ctx, n) <= 160 * 1024;
+}
+
+// santa_lb_kernel + santa_big_kernel over the blocks it left (out of its
+// lattice range; every block under SH_FLAG_TEST_RANGE / SH_FLAG_EXACT_ARGMIN).
+// The two list counters alternate between calls (launch_santa_sp's scheme).
+int launch_santa_lb(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
+  HIP_TRY_RC(ensure_ovf(ctx, B, s));
+  const int p = ctx->ovf_par;
+  a.ovf_cnt = ctx->d_ovf + p;
+  a.ovf_list = ctx->d_ovf + 2 + (size_t)p * ctx->ovf_cap;
+  a.blist = nullptr;
+  int rc = with_lb_cfg(a.n, [&](auto c) -> int {
+    using C = decltype(c);
+    static_assert(2 * C::NW + 2 <= 31, "the step word's table field");
+    const LbLds L = lb_lds_layout(a.n, ctx->ng, C::NW, C::K);
+    if (L.total > 160 * 1024) return fail(SH_ERR_ARGS, "staged-row kernel: LDS above 160 KiB");
+    static thread_local AttrCache attr;
+    if (L.total > 64 * 1024 && attr.need(ctx->device, L.total)) {
+      HIP_TRY(hipFuncSetAttribute((const void *)santa_lb_kernel<C::NW, C::K>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total));
+      attr.set(ctx->device, L.total);
+    }
+    if (a.flags & SH_FLAG_TIMING) {
+      if (L.total > 64 * 1024)
+        HIP_TRY(hipFuncSetAttribute((const void *)santa_lb_kernel<C::NW, C::K, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total));
+      hipLaunchKernelGGL((santa_lb_kernel<C::NW, C::K, true>), dim3(B), dim3(C::NW * WAVE), L.total, s, a);
+    } else {
+      hipLaunchKernelGGL((santa_lb_kernel<C::NW, C::K>), dim3(B), dim3(C::NW * WAVE), L.total, s, a);
+    }
+    HIP_TRY(hipGetLastError());
+    return SH_OK;
+  });
+  if (rc == SH_OK) {
+    SantaArgs f = a;
+    f.blist = a.ovf_list;
+    f.bcount = a.ovf_cnt;
+    f.ovf_reset = ctx->d_ovf + (p ^ 1);
+    rc = with_big_cfg<0>(ctx, a.n, 1, [&](auto c) {
+      using C = decltype(c);
+      return launch_big_cfg<0, C::NW, C::K, C::FB>(ctx, f, B, s);
+    });
+  }
+  if (rc) {
+    (void)hipMemsetAsync(ctx->d_ovf + p, 0, sizeof(int32_t), s);
+    return rc;
+  }
+  ctx->ovf_par = p ^ 1;
+  return SH_OK;
+}
+
+template <int MODE>
+int launch_santa_big(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
+  return with_big_cfg<MODE>(ctx, a.n, B, [&](auto c) {
+    using C = decltype(c);
+    return launch_big_cfg<MODE, C::NW, C::K, C::FB>(ctx, a, B, s);
+  });
+}
+
 
 // Register-tile 4-wave kernel in scaled units + the windowed-key launch over
 // the blocks it left (out of range; every block under the exact-argmin and
@@ -4980,6 +5457,7 @@ int vt_tile_slots(sh_ctx *ctx) {
 
 int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   // triplets (a few blocks per round: 1667 units) rebuild each row from the wishlists
+  if (n > 256 && mode == SH_MODE_SINGLE && lb_eligible(ctx, n, flags)) return SH_DESIGN_LARGE_LB;
   if (n > 256 || mode == SH_MODE_TRIPLETS) return SH_DESIGN_LARGE;
   // twins keep the LDS tile: their 128-dword register column does not stay
   // in VGPRs (the compiler moves it to scratch), and a round has 78 blocks
@@ -5034,6 +5512,12 @@ int resident_blocks(sh_ctx *ctx, int design, int mode, int n, int B) {
     case SH_DESIGN_LARGE:
       return mode == SH_MODE_SINGLE ? big_resident<0>(ctx, n, B)
              : mode == SH_MODE_TWINS ? big_resident<1>(ctx, n, B) : big_resident<2>(ctx, n, B);
+    case SH_DESIGN_LARGE_LB:
+      return with_lb_cfg(n, [&](auto c) {
+        using C = decltype(c);
+        return occ_blocks(ctx, santa_lb_kernel<C::NW, C::K>, C::NW * WAVE,
+                          lb_lds_layout(n, ctx->ng, C::NW, C::K).total);
+      });
     case SH_DESIGN_TWINS:
       return occ_blocks(ctx, santa_block_kernel<1, 1>, SANTA_WG, santa_lds_layout(n, 1, ctx->ng).total);
     case SH_DESIGN_LDS_TILE: return lds_tile_slots(ctx, n);
@@ -5075,6 +5559,7 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
       return mode == SH_MODE_SINGLE ? launch_santa_big<0>(ctx, a, B, s)
              : mode == SH_MODE_TWINS ? launch_santa_big<1>(ctx, a, B, s)
                                      : launch_santa_big<2>(ctx, a, B, s);
+    case SH_DESIGN_LARGE_LB: return launch_santa_lb(ctx, a, B, s);
     case SH_DESIGN_TWINS: return launch_santa<1, 1>(ctx, a, B, s);
     case SH_DESIGN_LDS_TILE:
       return (flags & SH_FLAG_TIMING) ? launch_santa<1, 0, true>(ctx, a, B, s) : launch_santa<1, 0>(ctx, a, B, s);

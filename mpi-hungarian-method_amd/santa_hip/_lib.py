@@ -32,9 +32,32 @@ SH_FLAG_TEST_RANGE = 512  # test hook: every register-tile block goes to the fal
 SH_FLAG_NO_APPLY = 1024  # solve without writing the gift types (overlapping blocks allowed)
 SH_FLAG_SP2 = 2048  # retired (round 4): the C-ABI refuses it (SH_ERR_ARGS)
 SH_FLAG_DT_TILE = 4096  # force the dense-tile one-wave kernel (santa_dt_kernel)
+SH_FLAG_BIG_ROWS = 8192  # singles n > 256: force the row-rebuild kernel (santa_big_kernel)
 SH_ERRF_ROWS = 1
 SH_ERRF_INFEASIBLE = 2
 SH_ERRF_TYPE = 4
+SH_DESIGN_SPARSE = 0
+SH_DESIGN_LDS_TILE = 1
+SH_DESIGN_SW_TILE = 2
+SH_DESIGN_VT_TILE = 3
+SH_DESIGN_TWINS = 4
+SH_DESIGN_LARGE = 5
+SH_DESIGN_SPARSE2 = 6
+SH_DESIGN_SPARSE3 = 7
+SH_DESIGN_DT_TILE = 8
+SH_DESIGN_LARGE_LB = 9
+SH_DESIGN_NAMES = {0: "santa_sp_kernel (1-wave sparse LDS tile)", 1: "santa_block_kernel (4-wave LDS byte tile)",
+                   2: "(retired: santa_sw_kernel)", 3: "santa_vt_kernel (4-wave register tile)",
+                   4: "santa_block_kernel (twins, 4-wave code-pair tile)",
+                   5: "santa_big_kernel (row rebuilt from the wishlist)",
+                   6: "(retired: santa_sp2_kernel)",
+                   7: "santa_sp3_kernel (1-wave sparse register tile built in-kernel, 32-bit lattice keys)",
+                   8: "santa_dt_kernel (LDS byte tile built by 4 waves, solved by 1 wave, 32-bit lattice keys)",
+                   9: "santa_lb_kernel (each wave's candidate row staged as a gift-type cost table in LDS, "
+                      "32-bit lattice keys)"}
+SH_MAX_N = 1024
+SH_MAX_N_SANTA = 4096
+
 _ERRF_TEXT = {SH_ERRF_ROWS: "a block's child ids out of [0, nc)",
               SH_ERRF_INFEASIBLE: "an infeasible solve",
               SH_ERRF_TYPE: "a block's current gift type out of [0, ng)"}
@@ -47,24 +70,7 @@ def describe_error_flags(flags: int) -> str:
     if rest:
         parts.append(f"unknown bits {rest:#x}")
     return "; ".join(parts) or "none"
-SH_DESIGN_SPARSE = 0
-SH_DESIGN_LDS_TILE = 1
-SH_DESIGN_SW_TILE = 2
-SH_DESIGN_VT_TILE = 3
-SH_DESIGN_TWINS = 4
-SH_DESIGN_LARGE = 5
-SH_DESIGN_SPARSE2 = 6
-SH_DESIGN_SPARSE3 = 7
-SH_DESIGN_DT_TILE = 8
-SH_DESIGN_NAMES = {0: "santa_sp_kernel (1-wave sparse LDS tile)", 1: "santa_block_kernel (4-wave LDS byte tile)",
-                   2: "(retired: santa_sw_kernel)", 3: "santa_vt_kernel (4-wave register tile)",
-                   4: "santa_block_kernel (twins, 4-wave code-pair tile)",
-                   5: "santa_big_kernel (row rebuilt from the wishlist)",
-                   6: "(retired: santa_sp2_kernel)",
-                   7: "santa_sp3_kernel (1-wave sparse register tile built in-kernel, 32-bit lattice keys)",
-                   8: "santa_dt_kernel (LDS byte tile built by 4 waves, solved by 1 wave, 32-bit lattice keys)"}
-SH_MAX_N = 1024
-SH_MAX_N_SANTA = 4096
+
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

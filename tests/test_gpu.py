@@ -209,6 +209,10 @@ def test_round_vs_oracle(sh, ctx, full_data, mode, n, B):
                      _lib.SH_FLAG_DT_TILE, _lib.SH_FLAG_DT_TILE | _lib.SH_FLAG_TEST_RANGE)
     elif mode == 1 and n <= 256:
         flag_sets = (0, _lib.SH_FLAG_TEST_RANGE)
+    elif mode == 0 and n <= 2048:
+        # the staged-row lattice kernel (default), the row-rebuild kernel
+        # (forced), and every block through the lattice kernel's fallback launch
+        flag_sets = (0, _lib.SH_FLAG_BIG_ROWS, _lib.SH_FLAG_TEST_RANGE)
     else:
         flag_sets = (0,)
     for fl in flag_sets:
@@ -401,14 +405,16 @@ def test_full_round_reference_block_sizes(sh, ctx, full_data, mode, n):
 
 @pytest.mark.parametrize("n", [300, 700, 1100, 2000])
 def test_large_block_wave_configs_agree(sh, ctx, full_data, n):
-    """Large blocks run 8 waves per block when a launch has at least one block
-    per CU and 16 otherwise: 260 blocks in one launch equal the same blocks in
-    launches of 65 (col, cost, steps, deltas, the new types), and two of them
-    equal the oracle."""
+    """The row-rebuild kernel runs 8 waves per block when a launch has at
+    least one block per CU and 16 otherwise: 260 blocks in one launch equal
+    the same blocks in launches of 65 (col, cost, steps, deltas, the new
+    types), and equal the staged-row lattice kernel's one launch (the
+    default); two of them equal the oracle."""
+    from santa_hip import _lib
     B = 260
     rows = ctx.sample_blocks(0, n, B, 11, 3)
     outs = []
-    for chunk in (B, 65):
+    for chunk, fl in ((B, _lib.SH_FLAG_BIG_ROWS), (65, _lib.SH_FLAG_BIG_ROWS), (B, 0)):
         types = ctx.upload_types(full_data.types)
         col = torch.empty(B * n, dtype=torch.int32, device="cuda")
         cost = torch.empty(B, dtype=torch.int64, device="cuda")
@@ -418,11 +424,12 @@ def test_large_block_wave_configs_agree(sh, ctx, full_data, n):
             sl = slice(b0 * n, (b0 + chunk) * n)
             d = torch.zeros(2, dtype=torch.int64, device="cuda")
             ctx.solve_blocks(0, rows[sl], n, types, col=col[sl], cost=cost[b0:b0 + chunk],
-                             steps=steps[b0:b0 + chunk], delta=d)
+                             steps=steps[b0:b0 + chunk], delta=d, flags=fl)
             delta += d
         outs.append([x.cpu().numpy() for x in (col, cost, steps, delta, types)])
-    for x, y in zip(*outs):
-        assert np.array_equal(x, y), n
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert np.array_equal(x, y), n
     assert ctx.error_flags() == 0
     r = rows.cpu().numpy().reshape(B, n)
     t_host = full_data.types.copy()
@@ -734,7 +741,11 @@ def test_design_dispatch(sh, ctx):
     # the register-tile design holds a whole round at once (4 waves per SIMD)
     assert ctx.resident_blocks(0, 256, 3730) >= 3730
     assert ctx.solve_design(1, 256, 78) == 4
-    assert ctx.solve_design(0, 2000, 477) == 5
+    assert ctx.solve_design(0, 2000, 477) == _lib.SH_DESIGN_LARGE_LB
+    assert ctx.solve_design(0, 2000, 1) == _lib.SH_DESIGN_LARGE_LB
+    assert ctx.resident_blocks(0, 2000, 477) >= 477  # (two blocks per CU: the round at once)
+    assert ctx.solve_design(0, 2000, 477, _lib.SH_FLAG_BIG_ROWS) == 5
+    assert ctx.solve_design(0, 4096, 1) == 5
     assert ctx.solve_design(1, 3000, 6) == 5
     assert ctx.solve_design(2, 256, 6) == 5
 

@@ -26,7 +26,7 @@ NO_SCRATCH = (
     "santa_tile_kernelILi1E",
     "santa_sp3_kernelILb0ELb0E", "santa_sp3_kernelILb0ELb1E", "santa_dt_kernel", "santa_vt_kernelILi0ELi1E", "santa_vt_kernelILi0ELi0E",
     "santa_block_kernelILi1ELi0ELb0E", "santa_block_kernelILi1ELi1ELb0E",
-    "santa_big_kernel", "score_kernel", "lsap_i64_kernel", "lsap_f64_kernel",
+    "santa_big_kernel", "santa_lb_kernel", "score_kernel", "lsap_i64_kernel", "lsap_f64_kernel",
 )
 
 

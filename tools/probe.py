@@ -28,6 +28,10 @@ def main():
     ap.add_argument("--segments", action="store_true",
                     help="santa_sp3_kernel: shader cycles per Dijkstra step by segment (A fetch+scatter+LDS, "
                          "B relax+argmin, C decode+book-keeping, D per-Dijkstra work per step)")
+    ap.add_argument("--lb-segments", action="store_true",
+                    help="santa_lb_kernel (n > 256 singles): cycles per step by segment, per wave "
+                         "(0 relax, 1 wave min, 2 candidate + staging + fold, 3 barrier, 4 decode, "
+                         "5 per-Dijkstra) and rows staged per step")
     ap.add_argument("--state-round", type=int, default=0,
                     help="time round R of the optimisation: first apply rounds 0..R-1 (default kernel)")
     a = ap.parse_args()
@@ -100,6 +104,21 @@ def main():
         out["segments_cycles_per_step"] = {nm: float(cv[:, q].sum() / sv.sum()) for q, nm in enumerate(names)}
         out["segments_cycles_per_step_maxblock"] = {nm: float(cv[imax, q] / sv[imax])
                                                     for q, nm in enumerate(names)}
+    if a.lb_segments:
+        t = base.clone()
+        col = torch.zeros(B * a.n, dtype=torch.int32, device="cuda")
+        ctx.solve_blocks(a.mode, rows, a.n, t, steps=steps, col=col, flags=_lib.SH_FLAG_TIMING | a.flags)
+        cv = col.view(B, a.n)[:, :128].cpu().numpy().astype(float).reshape(B, 16, 8)
+        sv = steps.cpu().numpy().astype(float)
+        nwv = int((cv[0, :, 0] > 0).sum())
+        names = ["relax", "wave_min", "candidate_stage_fold", "barrier", "decode_bookkeeping", "per_dijkstra"]
+        imax = int(sv.argmax())
+        out["lb_waves"] = nwv
+        out["lb_segments_cycles_per_step_maxblock"] = {
+            nm: [round(float(cv[imax, w, q] / sv[imax]), 1) for w in range(nwv)] for q, nm in enumerate(names)}
+        out["lb_staged_per_step_maxblock"] = [round(float(cv[imax, w, 6] / sv[imax]), 3) for w in range(nwv)]
+        out["lb_segments_mean_over_waves_all_blocks"] = {
+            nm: round(float(cv[:, :nwv, q].sum() / nwv / sv.sum()), 1) for q, nm in enumerate(names)}
     out["blocks"] = B
     out["n"] = a.n
     out["mode"] = a.mode
