@@ -178,7 +178,33 @@ def cpu_baselines(args, cpu: dict) -> dict:
     elif b1 is not None:
         cb["b1_error"] = b1.get("error")
     cb["timed"] = "before the GPU run, on the host cores this rank (or the launcher) leases"
+    cb["whole_node"] = whole_node_cpu(cb, cpu)
     return cb
+
+
+def whole_node_cpu(cb: dict, cpu: dict) -> dict:
+    """The CPU comparator of the whole host (every thread the machine has:
+    the reference's `mpirun -np <all cores>` on the node of an 8-GPU line),
+    projected from the figures measured on the leased cores: per-thread rate
+    x host threads.  The GPU box leases `used` of the host's threads and its
+    pool rules size worker pools to that share, so the whole node is not
+    timed; blocks of a round are independent (no communication inside a
+    solve), so linear scaling is an upper bound for the CPU -- it flatters
+    the CPU, never the GPU."""
+    used = max(int(cb.get("cores") or cpu.get("used") or 1), 1)
+    node = max(int(cpu.get("nproc") or used), used)
+    per = node / used
+    out = {"kind": "projected", "cores": node, "from_cores": used, "factor": round(per, 3),
+           "port_blocks_per_s": round(cb.get("value", 0.0) * per, 1),
+           "reference_lap_blocks_per_s": round(cb.get("reference_lap_blocks_per_s", 0.0) * per, 1),
+           "note": f"measured on {used} leased threads x {node}/{used}: linear scaling of independent "
+                   "blocks, an upper bound for the CPU"}
+    b1 = cb.get("b1_blocks_per_s") or {}
+    if b1:
+        p = max(b1, key=int)  # the largest P measured
+        out["b1_blocks_per_s"] = round(b1[p] * node / int(p), 2)
+        out["b1_from_procs"] = int(p)
+    return out
 
 
 def cpu_baseline(sd, mode: int, n: int, seconds: float, cores: int):

@@ -4270,7 +4270,7 @@ struct LbLds {
 __host__ __device__ __forceinline__ LbLds lb_lds_layout(int n, int ng, int nw, int k) {
   LbLds L;
   size_t o = 0;
-  L.TS = (ng + 1) & ~1;
+  L.TS = ((ng + 1) & ~1) + 2;  // (ng costs, then u of the row as an int32)
   L.u = o;     o += r16((size_t)n * 4);
   L.c4r = o;   o += r16((size_t)n * 2);
   L.r4c = o;   o += r16((size_t)n * 2);
@@ -4305,10 +4305,28 @@ struct LbRange {
 };
 
 // TIMED (dev, SH_FLAG_TIMING): every wave sums s_memtime cycles per segment of
-// its steps and writes them to col[b * n + 8 w + q]: 0 table reads + relaxation
-// + lane minimum, 1 wave DPP minimum, 2 candidate (readlanes, row staging, the
-// fold), 3 barrier, 4 word read + decode + book-keeping, 5 per-Dijkstra work,
-// 6 the number of rows this wave staged.
+// its steps and writes them to col[b * n + 8 w + q]: 0 pending row write +
+// relaxation + lane minimum, 1 wave DPP minimum, 2 candidate (readlanes,
+// synchronous row staging, the fold, the next candidate's prefetch), 3
+// barrier, 4 word read + decode + the next row's reads + book-keeping, 5
+// per-Dijkstra work, 6 rows staged synchronously, 7 rows prefetched.
+//
+// The step (wave w, columns j = (w K + k) 64 + lane):
+//   reads   c[k] = tbl[tb][type of j], u~ from the table's u entry (one LDS
+//           round trip, issued right after the previous step's decode)
+//   relax   r = W + c - u~ in key units, sbp = min(sbp, r << 12 | t), key
+//   argmin  lane min, wave DPP min -> the wave's candidate (lane, k by
+//           readlanes); an assigned candidate's row must be in one of the
+//           wave's two tables: usually it is (prefetched, below), else it is
+//           loaded now (the step's only dependent global load); the table's u
+//           entry gets u[row]; ds_min_u64 of the step word
+//   prefetch the wave's second-best candidate (the best among the other
+//           lanes' minima: the winning wave's next candidate is its previous
+//           second-best ~85 % of the time, tools/analysis/lb_stage_sim.py)
+//           is loaded into registers now and written into the wave's other
+//           table at the top of the next step, when no wave reads that table
+//   barrier, decode (SGPRs), the next step's reads, then the book-keeping
+//           (the winner leaves `remaining`, the mover's tie bits) in their shadow
 template <int NW, int K, bool TIMED = false>
 __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -4318,7 +4336,8 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n = a.n, nw = a.n_wish;
   const LbLds L = lb_lds_layout(n, a.ng, NW, K);
-  const int TS = L.TS;
+  const int TS = L.TS;         // table stride (int16 entries): ng costs, then u as int32
+  const int TU = (TS - 2) >> 1;  // the u entry's int32 index within a table
   int32_t *u32 = (int32_t *)(smem + L.u);
   int16_t *c4r = (int16_t *)(smem + L.c4r);
   int16_t *r4c_l = (int16_t *)(smem + L.r4c);
@@ -4328,6 +4347,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
   int32_t *rows_l = (int32_t *)(smem + L.rows);
   int16_t *ctype = (int16_t *)(smem + L.ctype);
   int16_t *tbl = (int16_t *)(smem + L.tbl);
+  int32_t *tbl32 = (int32_t *)(smem + L.tbl);
   uint64_t *words = (uint64_t *)(smem + L.words);
   int64_t *part = (int64_t *)(smem + L.part);
 
@@ -4352,10 +4372,10 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
     if (tid == 0) atomicOr(a.err, SH_ERRF_TYPE);
     return;
   }
-  {  // every table entry a miss (V = 1)
+  {  // every table entry a miss (V = 1), every u entry 0
     uint32_t *t32 = (uint32_t *)tbl;
     const int nd = (2 * NW + 2) * TS / 2;
-    for (int q = tid; q < nd; q += WG) t32[q] = 0x00010001u;
+    for (int q = tid; q < nd; q += WG) t32[q] = (q % (TS / 2) == TU) ? 0u : 0x00010001u;
   }
   for (int i = tid; i < n; i += WG) {
     u32[i] = 0;
@@ -4373,28 +4393,33 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
   int64_t steps = 0;
 
   if (!big && !(a.flags & SH_FLAG_BUILD_ONLY)) {
-    // per-thread columns j = (w * K + k) * 64 + lane
-    int ct[K];                 // the column's gift type (table index)
-    int32_t W[K];              // -v
-    uint32_t sbp[K], lo[K];    // path-step-tagged spc; tie bits (~0: left `remaining`)
-    int rc[K], crow[K];        // row4col, and that row's child id
+    int ct[K];               // the column's gift type (its cost's index in a table)
+    int32_t W[K];            // -v
+    uint32_t sbp[K], lo[K];  // path-step-tagged spc; tie bits (~0: left `remaining`)
+    uint32_t info[K];        // child of row4col << 11 | row4col (child < 2^20), ~0: unassigned
+    int32_t ucol[K];         // u of row4col
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       ct[k] = ctype[(w * K + k) * WAVE + lane];
       W[k] = 0;
     }
-    // tables 2w, 2w + 1 of this wave: the children they hold and, per lane,
-    // the two gifts this lane wrote there (g0 | g1 << 16; 0xFFFF none)
+    // this wave's tables 2w, 2w + 1: the children they hold and, per lane, the
+    // two gifts this lane wrote there (g0 | g1 << 16; 0xFFFF none)
     int chT0 = -1, chT1 = -1, lastSel = 0;
     uint32_t og0 = ~0u, og1 = ~0u;
-    // row cur's table (2 NW + (cur & 1)), staged by the last wave one
-    // Dijkstra ahead
+    // the prefetched row (child pch, for table 2w + pZ), held in registers
+    int pch = -1, pZ = 0, pg0 = -1, pg1 = -1;
+    // row cur's table 2 NW + (cur & 1): the last wave loads row cur + 1 at the
+    // start of Dijkstra cur and writes it at its end
     uint32_t ogC0 = ~0u, ogC1 = ~0u;
-    auto stage = [&](int slot, int child, uint32_t &ogs) {
-      int16_t *T = tbl + slot * TS;
+    int cg0 = -1, cg1 = -1;
+    auto load_row = [&](int child, int &g0, int &g1) {
       const int16_t *src = a.wish + (size_t)(uint32_t)child * (uint32_t)nw;
-      const int g0 = lane < nw ? src[lane] : -1;
-      const int g1 = lane + WAVE < nw ? src[lane + WAVE] : -1;
+      g0 = lane < nw ? src[lane] : -1;
+      g1 = lane + WAVE < nw ? src[lane + WAVE] : -1;
+    };
+    auto write_row = [&](int slot, int g0, int g1, uint32_t &ogs) {
+      int16_t *T = tbl + slot * TS;
       const uint32_t o0 = ogs & 0xFFFFu, o1 = ogs >> 16;
       if (o0 != 0xFFFFu) T[o0] = 1;  // (one wave: its clears land before its writes)
       if (o1 != 0xFFFFu) T[o1] = 1;
@@ -4402,12 +4427,16 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
       if (g1 >= 0) T[g1] = (int16_t)(-(nw - lane - WAVE) * 256);
       ogs = (uint32_t)(g0 & 0xFFFF) | ((uint32_t)(g1 & 0xFFFF) << 16);
     };
-    if (w == NW - 1) stage(2 * NW, rows_l[0], ogC0);
+    if (w == NW - 1) {
+      int g0, g1;
+      load_row(rows_l[0], g0, g1);
+      write_row(2 * NW, g0, g1, ogC0);
+    }
     __syncthreads();
     uint32_t accU = 0, accW = 0;
     int par = 0;  // rotating step word
     uint64_t seg[6] = {0, 0, 0, 0, 0, 0}, ts = 0;
-    uint32_t nstaged = 0;
+    uint32_t nsync = 0, npre = 0;
     auto stamp = [&](int q) {
       if constexpr (TIMED) {
         const uint64_t x = __builtin_amdgcn_s_memtime();
@@ -4421,15 +4450,20 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
       for (int k = 0; k < K; ++k) {
         const int j = (w * K + k) * WAVE + lane;
         const int rr = j < n ? r4c_l[j] : -1;
-        rc[k] = rr;
-        crow[k] = rr >= 0 ? rows_l[rr] : -1;
+        info[k] = rr >= 0 ? ((uint32_t)rows_l[rr] << 11) | (uint32_t)rr : ~0u;
+        ucol[k] = rr >= 0 ? u32[rr] : 0;
         const int p = n - 1 - j;
         lo[k] = j >= n ? ~0u : rr < 0 ? (uint32_t)(2047 - p) : (2048u | (uint32_t)p);
         sbp[k] = ~0u;
       }
+      if (w == NW - 1 && cur + 1 < n) load_row(rows_l[cur + 1], cg0, cg1);
       int nrem = n, t = 0, i = cur, sink = 0;
-      int32_t minVal = 0, ui = 0;
+      int32_t minVal = 0;
       int tb = 2 * NW + (cur & 1);
+      int32_t c[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) c[k] = tbl[tb * TS + ct[k]];
+      int32_t ui = 0;  // (u[cur] = 0: a row's first Dijkstra)
       stamp(5);
       for (;;) {
         ++steps;
@@ -4437,74 +4471,103 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
           rowq[t] = (int16_t)i;
           words[par == 2 ? 0 : par + 1] = ~0ull;  // re-arm the next step's word
         }
-        int32_t c[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) c[k] = tbl[tb * TS + ct[k]];
+        if (pch >= 0) {  // the prefetched row into its table (no wave reads it this step)
+          if (pZ == 0) {
+            write_row(2 * w, pg0, pg1, og0);
+            chT0 = pch;
+          } else {
+            write_row(2 * w + 1, pg0, pg1, og1);
+            chT1 = pch;
+          }
+          pch = -1;
+        }
         const int32_t ut = ui - minVal;
         accU |= (uint32_t)ut + R.CU;
         const uint32_t bse = (uint32_t)(LB_BIAS - ut);
+        uint32_t key[K];
         uint32_t best = ~0u;
-        int bk = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const uint32_t r = (uint32_t)W[k] + (uint32_t)c[k] + bse;
           sbp[k] = min(sbp[k], (r << LB_TSH) | (uint32_t)t);
-          const uint32_t key = (sbp[k] & ~((1u << LB_TSH) - 1u)) | lo[k];
-          const bool lt = key < best;
-          best = lt ? key : best;
-          bk = lt ? k : bk;
+          key[k] = (sbp[k] & ~((1u << LB_TSH) - 1u)) | lo[k];
+          best = min(best, key[k]);
         }
-        if constexpr (TIMED) asm volatile("" ::"v"(best), "v"(bk));
+        if constexpr (TIMED) asm volatile("" ::"v"(best));
         stamp(0);
         const uint32_t wmin = wave_min_u32_dpp(best);
         if constexpr (TIMED) asm volatile("" ::"s"(wmin));
         stamp(1);
         if (wmin != ~0u) {
-          const uint64_t bal = __builtin_amdgcn_ballot_w64(best == wmin);
-          const int wl = (int)__builtin_ctzll(bal);
-          const int kk = __builtin_amdgcn_readlane(bk, wl);
-          int rr = -1, ch = -1;
+          const int wl = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == wmin));
+          int kk = K - 1;
+#pragma unroll
+          for (int k = K - 2; k >= 0; --k)
+            if ((uint32_t)__builtin_amdgcn_readlane((int)key[k], wl) == wmin) kk = k;
+          uint32_t inf = 0;
+          int32_t uu = 0;
 #pragma unroll
           for (int k = 0; k < K; ++k)
             if (k == kk) {
-              rr = __builtin_amdgcn_readlane(rc[k], wl);
-              ch = __builtin_amdgcn_readlane(crow[k], wl);
+              inf = (uint32_t)__builtin_amdgcn_readlane((int)info[k], wl);
+              uu = __builtin_amdgcn_readlane(ucol[k], wl);
             }
           const int col = (w * K + kk) * WAVE + wl;
+          const bool asg = (wmin >> 11) & 1u;
           int slot = 0;
-          if (rr >= 0) {  // an assigned candidate: its row staged in one of this wave's tables
+          if (asg) {  // the candidate's row: staged in one of this wave's tables
+            const int ch = (int)(inf >> 11);
+            int v;
             if (ch == chT0) {
-              slot = 2 * w;
-              lastSel = 0;
+              v = 0;
             } else if (ch == chT1) {
-              slot = 2 * w + 1;
-              lastSel = 1;
-            } else {
-              int v = lastSel ^ 1;  // the table not used last, unless the step reads it
+              v = 1;
+            } else {  // not prefetched: load it now (on this step's chain)
+              v = lastSel ^ 1;  // the table not published last, unless the step reads it
               if (2 * w + v == tb) v ^= 1;
+              int g0, g1;
+              load_row(ch, g0, g1);
               if (v == 0) {
-                stage(2 * w, ch, og0);
+                write_row(2 * w, g0, g1, og0);
                 chT0 = ch;
               } else {
-                stage(2 * w + 1, ch, og1);
+                write_row(2 * w + 1, g0, g1, og1);
                 chT1 = ch;
               }
-              ++nstaged;
-              slot = 2 * w + v;
-              lastSel = v;
+              ++nsync;
             }
+            lastSel = v;
+            slot = 2 * w + v;
+            if (lane == 0) tbl32[slot * (TS >> 1) + TU] = uu;
           }
-          const uint64_t word = ((uint64_t)wmin << 32) | ((uint32_t)col << 16) |
-                                ((uint32_t)(rr & 0x7FF) << 5) | (uint32_t)slot;
+          const uint64_t word = ((uint64_t)wmin << 32) | ((uint32_t)col << 16) | ((inf & 0x7FFu) << 5) |
+                                (uint32_t)slot;
           if (lane == 0)
             __hip_atomic_fetch_min(words + par, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          // the wave's next candidate, most likely: the best among the other lanes
+          const uint32_t wmin2 = wave_min_u32_dpp(lane == wl ? ~0u : best);
+          if (wmin2 != ~0u && ((wmin2 >> 11) & 1u)) {
+            const int wl2 = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == wmin2));
+            int kk2 = K - 1;
+#pragma unroll
+            for (int k = K - 2; k >= 0; --k)
+              if ((uint32_t)__builtin_amdgcn_readlane((int)key[k], wl2) == wmin2) kk2 = k;
+            uint32_t inf2 = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+              if (k == kk2) inf2 = (uint32_t)__builtin_amdgcn_readlane((int)info[k], wl2);
+            const int ch2 = (int)(inf2 >> 11);
+            if (ch2 != chT0 && ch2 != chT1) {
+              // into the table this step did not publish (written at the top
+              // of the next step, which reads the winner's table: not this one)
+              pZ = asg ? (slot & 1) ^ 1 : lastSel ^ 1;
+              pch = ch2;
+              load_row(ch2, pg0, pg1);
+              ++npre;
+            }
+          }
         }
-        // row cur + 1, staged during Dijkstra cur's first step
-        if (t == 0 && w == NW - 1 && cur + 1 < n) {
-          if ((cur + 1) & 1) stage(2 * NW + 1, rows_l[cur + 1], ogC1);
-          else stage(2 * NW, rows_l[cur + 1], ogC0);
-        }
-        if constexpr (TIMED) __builtin_amdgcn_s_waitcnt(0);
+        if constexpr (TIMED) __builtin_amdgcn_s_waitcnt(0xC07F);  // (lgkmcnt(0): the LDS writes)
         stamp(2);
         __syncthreads();
         stamp(3);
@@ -4522,6 +4585,13 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         const int pk = (int)(gk & 2047u);
         const int pstar = assigned ? pk : 2047 - pk;
         const int gcol = (int)(gl >> 16);
+        if (assigned) {  // the next step's row: its reads first
+          i = (int)((gl >> 5) & 0x7FFu);
+          tb = (int)(gl & 31u);
+#pragma unroll
+          for (int k = 0; k < K; ++k) c[k] = tbl[tb * TS + ct[k]];
+          ui = tbl32[tb * (TS >> 1) + TU];
+        }
         // book-keeping: the winner leaves `remaining`, the column at position
         // `last` takes position pstar (its tie bits flip by last ^ pstar)
 #pragma unroll
@@ -4536,14 +4606,26 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
           sink = gcol;
           break;
         }
-        i = (int)((gl >> 5) & 0x7FFu);
-        tb = (int)(gl & 31u);
-        ui = u32[i];
-        if constexpr (TIMED) asm volatile("" ::"s"(ui));
+        if constexpr (TIMED) asm volatile("" ::"v"(c[0]), "s"(ui));
         stamp(4);
       }
       stamp(4);
       if (big) break;  // (block-uniform: every wave read the same word)
+      // the rows loaded during the Dijkstra into their tables (none is read now)
+      if (pch >= 0) {
+        if (pZ == 0) {
+          write_row(2 * w, pg0, pg1, og0);
+          chT0 = pch;
+        } else {
+          write_row(2 * w + 1, pg0, pg1, og1);
+          chT1 = pch;
+        }
+        pch = -1;
+      }
+      if (w == NW - 1 && cur + 1 < n) {
+        if ((cur + 1) & 1) write_row(2 * NW + 1, cg0, cg1, ogC1);
+        else write_row(2 * NW, cg0, cg1, ogC0);
+      }
       // dual update of the visited columns and their rows, path rows
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -4551,7 +4633,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         if (j < n && lo[k] == ~0u) {
           const int32_t d = minVal - ((int32_t)(sbp[k] >> LB_TSH) - LB_BIAS);
           W[k] += d;
-          if (rc[k] >= 0) u32[rc[k]] += d;
+          if (!(info[k] >> 31)) u32[info[k] & 0x7FFu] += d;
           path_l[j] = rowq[sbp[k] & ((1u << LB_TSH) - 1u)];
         }
         if (j < n) accW |= (uint32_t)W[k] + R.CW;
@@ -4578,7 +4660,8 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
       if (lane == 0 && a.col) {
         int32_t *o = a.col + (size_t)b * n + 8 * w;
         for (int q = 0; q < 6; ++q) o[q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
-        o[6] = (int32_t)nstaged;
+        o[6] = (int32_t)nsync;
+        o[7] = (int32_t)npre;
       }
     }
     big |= (accU & R.MU) != 0 || (accW & R.MW) != 0;
@@ -5207,9 +5290,11 @@ size_t lb_lds_bytes(const sh_ctx *ctx, int n) {
 }
 
 // singles blocks the staged-row lattice kernel takes: 256 < n <= 2048 whose
-// LDS fits (the tables hold ng int16 entries each)
+// LDS fits (the tables hold ng int16 entries each), child ids below 2^20 (a
+// column's row and child share one 31-bit register)
 bool lb_eligible(const sh_ctx *ctx, int n, unsigned flags) {
-  return n > 256 && n <= LB_MAX_N && !(flags & SH_FLAG_BIG_ROWS) && lb_lds_bytes(ctx, n) <= 160 * 1024;
+  return n > 256 && n <= LB_MAX_N && ctx->nc <= (1 << 20) && !(flags & SH_FLAG_BIG_ROWS) &&
+         lb_lds_bytes(ctx, n) <= 160 * 1024;
 }
 
 // santa_lb_kernel + santa_big_kernel over the blocks it left (out of its

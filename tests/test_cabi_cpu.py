@@ -273,3 +273,21 @@ def test_error_flags_are_described_by_bit():
     both = _lib.describe_error_flags(_lib.SH_ERRF_TYPE | _lib.SH_ERRF_INFEASIBLE)
     assert "gift type" in both and "infeasible" in both and "child ids" not in both
     assert "unknown bits 0x10" in _lib.describe_error_flags(0x10)
+
+
+def test_bench_whole_node_cpu_projection():
+    """bench.py's whole-host CPU comparator: the leased-core figures scaled by
+    host threads / leased threads (B1 from its largest measured P)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    cb = {"value": 100.0, "cores": 16, "reference_lap_blocks_per_s": 50.0,
+          "b1_blocks_per_s": {"8": 4.0, "16": 8.0}}
+    wn = bench.whole_node_cpu(cb, {"nproc": 256, "used": 16})
+    assert wn["cores"] == 256 and wn["from_cores"] == 16 and wn["factor"] == 16.0
+    assert wn["port_blocks_per_s"] == 1600.0 and wn["reference_lap_blocks_per_s"] == 800.0
+    assert wn["b1_blocks_per_s"] == 128.0 and wn["b1_from_procs"] == 16
+    # a host with no more threads than leased: the measured figures themselves
+    wn = bench.whole_node_cpu(cb, {"nproc": 8, "used": 16})
+    assert wn["cores"] == 16 and wn["port_blocks_per_s"] == 100.0

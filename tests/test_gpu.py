@@ -937,6 +937,10 @@ def test_bench_launches_n_ranks(sh):
     cb = line["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
     assert set(cb["b1_blocks_per_s"]) and all(v > 0 for v in cb["b1_blocks_per_s"].values())
+    # the whole-host comparator beside the leased-core figures
+    wn = cb["whole_node"]
+    assert wn["cores"] >= cb["cores"] and wn["port_blocks_per_s"] >= cb["value"]
+    assert wn["b1_blocks_per_s"] > 0 and wn["kind"] == "projected"
     # rank 0's shard carries HBM traffic from a PMC summary of the same launch size, or says why not
     roof = line["roofline"]
     assert roof.get("traffic") is not None or roof.get("traffic_note"), roof

@@ -117,6 +117,7 @@ def main():
         out["lb_segments_cycles_per_step_maxblock"] = {
             nm: [round(float(cv[imax, w, q] / sv[imax]), 1) for w in range(nwv)] for q, nm in enumerate(names)}
         out["lb_staged_per_step_maxblock"] = [round(float(cv[imax, w, 6] / sv[imax]), 3) for w in range(nwv)]
+        out["lb_prefetched_per_step_maxblock"] = [round(float(cv[imax, w, 7] / sv[imax]), 3) for w in range(nwv)]
         out["lb_segments_mean_over_waves_all_blocks"] = {
             nm: round(float(cv[:, :nwv, q].sum() / nwv / sv.sum()), 1) for q, nm in enumerate(names)}
     out["blocks"] = B
