@@ -4254,12 +4254,25 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
 // scipy's strict <, the path row is rowq[t]); key = sbp & ~0xFFF | tie, tie =
 // class 1 | pkey 11 (scipy's order among equal values: the last unassigned
 // column in `remaining`, else the first).  The step word folded with ds_min_u64
-// is key << 32 | column << 16 | row4col << 5 | table.  Range (the boxes of
+// is key << 32 | column << 17 | row4col << 6 | table.  Range (the boxes of
 // LatticeRange in base 256): u~ = u - minVal |A| < 1024, |m| <= 2^bU; W = -v
 // |A| < 512, |m| <= 2^cW, 2^cW + 1 + 2^bU <= 127, so every relaxation value
 // has |V| < 2^19; a block that leaves them is left untouched and re-solved by
 // santa_big_kernel (the fallback launch over its list).
 // ---------------------------------------------------------------------------
+// A/B switches (round 5, profiles/r05f_lb_ab.jsonl): prefetching each wave's
+// second-best candidate row doubled the synchronous loads' latency (640 ->
+// 1,270 cycles for a lone block) and lost 25-38 %; the one-line packed rows
+// lost 6-7 % to the int16 rows (four loads and a decode per gift pair)
+#ifndef LB_PREFETCH
+#define LB_PREFETCH 0
+#endif
+#ifndef LB_PACKED
+#define LB_PACKED 0
+#endif
+#ifndef LB_CFG_2048
+#define LB_CFG_2048 0  // 1024 < n <= 2048: 0 = 8 waves x 4 columns, 1 = 4 x 8, 2 = 16 x 2
+#endif
 constexpr int LB_TSH = 12;                 // sbp's step field and the key's tie field
 constexpr int32_t LB_BIAS = 1 << 19;       // spc_V + BIAS in [0, 2^20)
 constexpr int LB_MAX_N = 2048;             // 11-bit positions
@@ -4270,7 +4283,7 @@ struct LbLds {
 __host__ __device__ __forceinline__ LbLds lb_lds_layout(int n, int ng, int nw, int k) {
   LbLds L;
   size_t o = 0;
-  L.TS = ((ng + 1) & ~1) + 2;  // (ng costs, then u of the row as an int32)
+  L.TS = ((ng + 1) & ~1) + 64 + 2;  // (ng costs, a dump entry per lane, then u of the row as an int32)
   L.u = o;     o += r16((size_t)n * 4);
   L.c4r = o;   o += r16((size_t)n * 2);
   L.r4c = o;   o += r16((size_t)n * 2);
@@ -4333,11 +4346,13 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
   constexpr int WG = NW * WAVE;
   constexpr int NCOL = WG * K;
   const int b = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: SGPR arithmetic below)
   const int n = a.n, nw = a.n_wish;
   const LbLds L = lb_lds_layout(n, a.ng, NW, K);
   const int TS = L.TS;         // table stride (int16 entries): ng costs, then u as int32
   const int TU = (TS - 2) >> 1;  // the u entry's int32 index within a table
+  const int DUMP = TS - 2 - 64;    // lane l's dump entry: DUMP + l (a row write with no exec mask)
   int32_t *u32 = (int32_t *)(smem + L.u);
   int16_t *c4r = (int16_t *)(smem + L.c4r);
   int16_t *r4c_l = (int16_t *)(smem + L.r4c);
@@ -4406,26 +4421,45 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
     // this wave's tables 2w, 2w + 1: the children they hold and, per lane, the
     // two gifts this lane wrote there (g0 | g1 << 16; 0xFFFF none)
     int chT0 = -1, chT1 = -1, lastSel = 0;
-    uint32_t og0 = ~0u, og1 = ~0u;
+    const uint32_t ogd = (uint32_t)(DUMP + lane) * 0x10001u;  // (both gifts at the lane's dump entry)
+    uint32_t og0 = ogd, og1 = ogd;
     // the prefetched row (child pch, for table 2w + pZ), held in registers
     int pch = -1, pZ = 0, pg0 = -1, pg1 = -1;
     // row cur's table 2 NW + (cur & 1): the last wave loads row cur + 1 at the
     // start of Dijkstra cur and writes it at its end
-    uint32_t ogC0 = ~0u, ogC1 = ~0u;
+    uint32_t ogC0 = ogd, ogC1 = ogd;
     int cg0 = -1, cg1 = -1;
+    // a row's gifts: lane l holds ranks l and l + 64 (-1 past n_wish); from
+    // the packed line (gift r at bits 10 r .. 10 r + 9: one 128-byte line, one
+    // request) or the int16 row (200 bytes over two or three lines)
+    const bool packed = LB_PACKED && a.wish10 != nullptr;
     auto load_row = [&](int child, int &g0, int &g1) {
-      const int16_t *src = a.wish + (size_t)(uint32_t)child * (uint32_t)nw;
-      g0 = lane < nw ? src[lane] : -1;
-      g1 = lane + WAVE < nw ? src[lane + WAVE] : -1;
+      if (packed) {
+        const uint32_t *line = a.wish10 + (size_t)(uint32_t)child * 32u;
+        const uint32_t b0 = 10u * (uint32_t)lane, b1 = 10u * (uint32_t)(lane + WAVE);
+        const bool v0 = lane < nw, v1 = lane + WAVE < nw;
+        const uint32_t d0 = b0 >> 5, d1 = v1 ? (b1 >> 5) : 0u;
+        const uint32_t x0 = v0 ? line[d0] : 0u, y0 = v0 ? line[min(d0 + 1u, 31u)] : 0u;
+        const uint32_t x1 = v1 ? line[d1] : 0u, y1 = v1 ? line[min(d1 + 1u, 31u)] : 0u;
+        g0 = v0 ? (int)(__builtin_amdgcn_alignbit(y0, x0, b0 & 31u) & 1023u) : -1;
+        g1 = v1 ? (int)(__builtin_amdgcn_alignbit(y1, x1, b1 & 31u) & 1023u) : -1;
+      } else {
+        const int16_t *src = a.wish + (size_t)(uint32_t)child * (uint32_t)nw;
+        g0 = lane < nw ? src[lane] : -1;
+        g1 = lane + WAVE < nw ? src[lane + WAVE] : -1;
+      }
     };
+    // (a lane with no gift writes its dump entry: four stores with no exec
+    // masking; one wave: its clears land before its writes)
     auto write_row = [&](int slot, int g0, int g1, uint32_t &ogs) {
       int16_t *T = tbl + slot * TS;
-      const uint32_t o0 = ogs & 0xFFFFu, o1 = ogs >> 16;
-      if (o0 != 0xFFFFu) T[o0] = 1;  // (one wave: its clears land before its writes)
-      if (o1 != 0xFFFFu) T[o1] = 1;
-      if (g0 >= 0) T[g0] = (int16_t)(-(nw - lane) * 256);
-      if (g1 >= 0) T[g1] = (int16_t)(-(nw - lane - WAVE) * 256);
-      ogs = (uint32_t)(g0 & 0xFFFF) | ((uint32_t)(g1 & 0xFFFF) << 16);
+      T[ogs & 0xFFFFu] = 1;
+      T[ogs >> 16] = 1;
+      const uint32_t e0 = g0 >= 0 ? (uint32_t)g0 : (uint32_t)(DUMP + lane);
+      const uint32_t e1 = g1 >= 0 ? (uint32_t)g1 : (uint32_t)(DUMP + lane);
+      T[e0] = (int16_t)(-(nw - lane) * 256);
+      T[e1] = (int16_t)(-(nw - lane - WAVE) * 256);
+      ogs = e0 | (e1 << 16);
     };
     if (w == NW - 1) {
       int g0, g1;
@@ -4435,7 +4469,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
     __syncthreads();
     uint32_t accU = 0, accW = 0;
     int par = 0;  // rotating step word
-    uint64_t seg[6] = {0, 0, 0, 0, 0, 0}, ts = 0;
+    uint64_t seg[6] = {0, 0, 0, 0, 0, 0}, ts = 0, ldlat = 0;
     uint32_t nsync = 0, npre = 0;
     auto stamp = [&](int q) {
       if constexpr (TIMED) {
@@ -4466,6 +4500,20 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
       int32_t ui = 0;  // (u[cur] = 0: a row's first Dijkstra)
       stamp(5);
       for (;;) {
+        // (the loop-carried scalars are wave-uniform: kept in SGPRs, so the
+        // candidate logic below branches on the scalar unit)
+        tb = __builtin_amdgcn_readfirstlane(tb);
+        i = __builtin_amdgcn_readfirstlane(i);
+        t = __builtin_amdgcn_readfirstlane(t);
+        nrem = __builtin_amdgcn_readfirstlane(nrem);
+        par = __builtin_amdgcn_readfirstlane(par);
+        minVal = __builtin_amdgcn_readfirstlane(minVal);
+        ui = __builtin_amdgcn_readfirstlane(ui);
+        chT0 = __builtin_amdgcn_readfirstlane(chT0);
+        chT1 = __builtin_amdgcn_readfirstlane(chT1);
+        lastSel = __builtin_amdgcn_readfirstlane(lastSel);
+        pch = __builtin_amdgcn_readfirstlane(pch);
+        pZ = __builtin_amdgcn_readfirstlane(pZ);
         ++steps;
         if (tid == 0) {
           rowq[t] = (int16_t)i;
@@ -4515,6 +4563,9 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
           const int col = (w * K + kk) * WAVE + wl;
           const bool asg = (wmin >> 11) & 1u;
           int slot = 0;
+          bool sync = false;
+          int sg0 = -1, sg1 = -1;
+          uint64_t tl = 0;
           if (asg) {  // the candidate's row: staged in one of this wave's tables
             const int ch = (int)(inf >> 11);
             int v;
@@ -4522,29 +4573,27 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
               v = 0;
             } else if (ch == chT1) {
               v = 1;
-            } else {  // not prefetched: load it now (on this step's chain)
+            } else {  // not staged: load it now (on this step's chain)
               v = lastSel ^ 1;  // the table not published last, unless the step reads it
               if (2 * w + v == tb) v ^= 1;
-              int g0, g1;
-              load_row(ch, g0, g1);
-              if (v == 0) {
-                write_row(2 * w, g0, g1, og0);
-                chT0 = ch;
-              } else {
-                write_row(2 * w + 1, g0, g1, og1);
-                chT1 = ch;
-              }
+              if constexpr (TIMED) tl = __builtin_amdgcn_s_memtime();
+              load_row(ch, sg0, sg1);
+              if (v == 0) chT0 = ch;
+              else chT1 = ch;
+              sync = true;
               ++nsync;
             }
             lastSel = v;
             slot = 2 * w + v;
             if (lane == 0) tbl32[slot * (TS >> 1) + TU] = uu;
           }
-          const uint64_t word = ((uint64_t)wmin << 32) | ((uint32_t)col << 16) | ((inf & 0x7FFu) << 5) |
+          const uint64_t word = ((uint64_t)wmin << 32) | ((uint32_t)col << 17) | ((inf & 0x7FFu) << 6) |
                                 (uint32_t)slot;
           if (lane == 0)
             __hip_atomic_fetch_min(words + par, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          // the wave's next candidate, most likely: the best among the other lanes
+#if LB_PREFETCH
+          // the wave's next candidate, most likely: the best among the other
+          // lanes (computed while the synchronous load is in flight)
           const uint32_t wmin2 = wave_min_u32_dpp(lane == wl ? ~0u : best);
           if (wmin2 != ~0u && ((wmin2 >> 11) & 1u)) {
             const int wl2 = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == wmin2));
@@ -4566,6 +4615,15 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
               ++npre;
             }
           }
+#endif
+          if (sync) {  // the synchronous row into its table before the barrier
+            if constexpr (TIMED) {
+              asm volatile("" ::"v"(sg0), "v"(sg1));
+              ldlat += __builtin_amdgcn_s_memtime() - tl;
+            }
+            if ((slot & 1) == 0) write_row(slot, sg0, sg1, og0);
+            else write_row(slot, sg0, sg1, og1);
+          }
         }
         if constexpr (TIMED) __builtin_amdgcn_s_waitcnt(0xC07F);  // (lgkmcnt(0): the LDS writes)
         stamp(2);
@@ -4573,9 +4631,11 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         stamp(3);
         const uint64_t g = words[par];
         const int last = nrem - 1;
-        const int mcol = rem[last];
+        const int mcol = __builtin_amdgcn_readfirstlane((int)rem[last]);
         par = par == 2 ? 0 : par + 1;
-        const uint32_t gk = (uint32_t)(g >> 32), gl = (uint32_t)g;
+        // (the word is block-uniform: decoded in SGPRs, the branches below scalar)
+        const uint32_t gk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32));
+        const uint32_t gl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
         if (gk == ~0u) {  // no live column left without a sink: only from values out of range
           big = true;
           break;
@@ -4584,20 +4644,34 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         const bool assigned = (gk >> 11) & 1u;
         const int pk = (int)(gk & 2047u);
         const int pstar = assigned ? pk : 2047 - pk;
-        const int gcol = (int)(gl >> 16);
+        const int gcol = (int)(gl >> 17);
         if (assigned) {  // the next step's row: its reads first
-          i = (int)((gl >> 5) & 0x7FFu);
-          tb = (int)(gl & 31u);
+          i = (int)((gl >> 6) & 0x7FFu);
+          tb = (int)(gl & 63u);
 #pragma unroll
           for (int k = 0; k < K; ++k) c[k] = tbl[tb * TS + ct[k]];
-          ui = tbl32[tb * (TS >> 1) + TU];
+          ui = __builtin_amdgcn_readfirstlane(tbl32[tb * (TS >> 1) + TU]);
         }
-        // book-keeping: the winner leaves `remaining`, the column at position
-        // `last` takes position pstar (its tie bits flip by last ^ pstar)
+        // book-keeping, one lane each in the owner wave: the winner leaves
+        // `remaining`, the column at position `last` takes position pstar (its
+        // tie bits flip by last ^ pstar)
+        constexpr int KSH = K == 1 ? 0 : K == 2 ? 1 : K == 4 ? 2 : 3;
+        static_assert((1 << KSH) == K, "K a power of two <= 8");
+        if ((gcol >> (6 + KSH)) == w) {
+          const int kg = (gcol >> 6) & (K - 1), lg = gcol & 63;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const int j = (w * K + k) * WAVE + lane;
-          lo[k] = (j == gcol) ? ~0u : (j == mcol && pstar != last) ? (lo[k] ^ (uint32_t)(last ^ pstar)) : lo[k];
+          for (int k = 0; k < K; ++k)
+            if (k == kg) asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(lo[k]) : "s"(~0u), "{m0}"(lg));
+        }
+        if (pstar != last && (mcol >> (6 + KSH)) == w) {
+          const int km = (mcol >> 6) & (K - 1), lm = mcol & 63;
+          const uint32_t kX = (uint32_t)(last ^ pstar);
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+            if (k == km) {
+              const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)lo[k], lm) ^ kX;
+              asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(lo[k]) : "s"(x), "{m0}"(lm));
+            }
         }
         if (tid == 0 && pstar != last) rem[pstar] = (int16_t)mcol;
         nrem = last;
@@ -4662,6 +4736,8 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         for (int q = 0; q < 6; ++q) o[q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
         o[6] = (int32_t)nsync;
         o[7] = (int32_t)npre;
+        // (the synchronous loads' latency, issue to data, in col[b * n + 128 + w])
+        a.col[(size_t)b * n + 128 + w] = (int32_t)min(ldlat, (uint64_t)INT32_MAX);
       }
     }
     big |= (accU & R.MU) != 0 || (accW & R.MW) != 0;
@@ -5274,12 +5350,18 @@ int ensure_ovf(sh_ctx *ctx, int B, hipStream_t s) {
 }
 
 // santa_lb_kernel's configuration for n (NW * 64 * K >= n columns; the word's
-// table field holds 2 NW + 2 <= 31 tables)
+// table field holds 2 NW + 2 <= 63 tables)
 template <typename F>
 int with_lb_cfg(int n, F &&f) {
   if (n <= 512) return f(BigCfg<2, 4, 0>{});
   if (n <= 1024) return f(BigCfg<4, 4, 0>{});
+#if LB_CFG_2048 == 1
+  return f(BigCfg<4, 8, 0>{});
+#elif LB_CFG_2048 == 2
+  return f(BigCfg<16, 2, 0>{});
+#else
   return f(BigCfg<8, 4, 0>{});
+#endif
 }
 
 size_t lb_lds_bytes(const sh_ctx *ctx, int n) {
@@ -5308,7 +5390,7 @@ int launch_santa_lb(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   a.blist = nullptr;
   int rc = with_lb_cfg(a.n, [&](auto c) -> int {
     using C = decltype(c);
-    static_assert(2 * C::NW + 2 <= 31, "the step word's table field");
+    static_assert(2 * C::NW + 2 <= 63, "the step word's table field");
     const LbLds L = lb_lds_layout(a.n, ctx->ng, C::NW, C::K);
     if (L.total > 160 * 1024) return fail(SH_ERR_ARGS, "staged-row kernel: LDS above 160 KiB");
     static thread_local AttrCache attr;

@@ -14,6 +14,7 @@ for f in ("r5c_lone", "r5c_round0", "r5c_round10"):
         print("  ", k, v)
     print("   staged", d["lb_staged_per_step_maxblock"])
     print("   prefetched", d.get("lb_prefetched_per_step_maxblock"))
+    print("   sync load cycles", d.get("lb_sync_load_cycles_maxblock"))
     print("   mean", d["lb_segments_mean_over_waves_all_blocks"])
 PY
 echo all-done

@@ -108,7 +108,9 @@ def main():
         t = base.clone()
         col = torch.zeros(B * a.n, dtype=torch.int32, device="cuda")
         ctx.solve_blocks(a.mode, rows, a.n, t, steps=steps, col=col, flags=_lib.SH_FLAG_TIMING | a.flags)
-        cv = col.view(B, a.n)[:, :128].cpu().numpy().astype(float).reshape(B, 16, 8)
+        cfull = col.view(B, a.n).cpu().numpy().astype(float)
+        cv = cfull[:, :128].reshape(B, 16, 8)
+        lat = cfull[:, 128:144]
         sv = steps.cpu().numpy().astype(float)
         nwv = int((cv[0, :, 0] > 0).sum())
         names = ["relax", "wave_min", "candidate_stage_fold", "barrier", "decode_bookkeeping", "per_dijkstra"]
@@ -118,6 +120,8 @@ def main():
             nm: [round(float(cv[imax, w, q] / sv[imax]), 1) for w in range(nwv)] for q, nm in enumerate(names)}
         out["lb_staged_per_step_maxblock"] = [round(float(cv[imax, w, 6] / sv[imax]), 3) for w in range(nwv)]
         out["lb_prefetched_per_step_maxblock"] = [round(float(cv[imax, w, 7] / sv[imax]), 3) for w in range(nwv)]
+        out["lb_sync_load_cycles_maxblock"] = [round(float(lat[imax, w] / max(cv[imax, w, 6], 1)), 1)
+                                               for w in range(nwv)]
         out["lb_segments_mean_over_waves_all_blocks"] = {
             nm: round(float(cv[:, :nwv, q].sum() / nwv / sv.sum()), 1) for q, nm in enumerate(names)}
     out["blocks"] = B
