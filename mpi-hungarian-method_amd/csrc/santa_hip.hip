@@ -20,6 +20,22 @@
 #include "santa_hip.h"
 #include "sh_common.h"
 
+// Build-time A/B switches (round 5; santa_lb_kernel: profiles/r05f_lb_ab.jsonl): prefetching each wave's
+// second-best candidate row doubled the synchronous loads' latency (640 ->
+// 1,270 cycles for a lone block) and lost 25-38 %; the one-line packed rows
+// lost 6-7 % to the int16 rows (four loads and a decode per gift pair)
+#ifndef LB_PREFETCH
+#define LB_PREFETCH 0
+#endif
+#ifndef SP3_MASKED_DUAL
+#define SP3_MASKED_DUAL 1  // santa_sp3_kernel's dual update: the visited columns only (exec-masked)
+#endif
+#ifndef LB_PACKED
+#define LB_PACKED 0
+#endif
+#ifndef LB_CFG_2048
+#define LB_CFG_2048 0  // 1024 < n <= 2048: 0 = 8 waves x 4 columns, 1 = 4 x 8, 2 = 16 x 2
+#endif
 namespace {
 
 constexpr int WAVE = 64;
@@ -3523,6 +3539,21 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       // unreached column reads an unused in-bounds word).
       const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
       i32x4 prow;  // (one VGPR tuple: the augmentation selects prow[j & 3] by an indexed move)
+#if SP3_MASKED_DUAL  // (the visited columns and the sink only; 1 % faster here,
+                     //  2-4 % slower in santa_dt_kernel: profiles/r05h_masked_dual_ab.jsonl)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool vk = (lo[k] == ~0u || 4 * lane + k == sink) && (4 * lane + k < n);
+        if (vk) {
+          const int32_t dd = (int32_t)(mvb - (sbp[k] >> SP3_SH));
+          W[k] += dd;
+          Wp[k] = (int32_t)((uint32_t)W[k] << SP3_SH);
+          __hip_atomic_fetch_add(u_l + ((r4c >> (8 * k)) & 0xFFu), dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
+        }
+        accW |= (uint32_t)W[k] + LR.CW;
+      }
+#else
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
@@ -3534,6 +3565,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
       }
+#endif
       if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       // the sink is the one column this Dijkstra assigns
       {  // the sink is the one column this Dijkstra assigns: flip its start tie bits
@@ -3855,6 +3887,24 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       // dual update, path rows, augmentation: santa_sp3_kernel's
       const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
       i32x4 prow;
+#ifdef DT_MASKED_DUAL
+      // (dev, DESIGN §4.0b: round 4's exec-masked variant = 1, which skipped
+      // the sink's path row -- the sink's removal is deferred, so its lo is
+      // not ~0 here -- and sent every block to the fallback launch; 2 = the
+      // same with the sink included)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool vk = (lo[k] == ~0u || (DT_MASKED_DUAL == 2 && 4 * lane + k == sink)) && (4 * lane + k < n);
+        if (vk) {
+          const int32_t dd = (int32_t)(mvb - (sbp[k] >> SP3_SH));
+          W[k] += dd;
+          Wp[k] = (int32_t)((uint32_t)W[k] << SP3_SH);
+          __hip_atomic_fetch_add(u_l + ((r4c >> (8 * k)) & 0xFFu), dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
+        }
+        accW |= (uint32_t)W[k] + LR.CW;
+      }
+#else
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
@@ -3866,6 +3916,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
       }
+#endif
       if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       {  // the sink is the one column this Dijkstra assigns: flip its start tie bits
         uint64_t sv;
@@ -4260,19 +4311,6 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
 // has |V| < 2^19; a block that leaves them is left untouched and re-solved by
 // santa_big_kernel (the fallback launch over its list).
 // ---------------------------------------------------------------------------
-// A/B switches (round 5, profiles/r05f_lb_ab.jsonl): prefetching each wave's
-// second-best candidate row doubled the synchronous loads' latency (640 ->
-// 1,270 cycles for a lone block) and lost 25-38 %; the one-line packed rows
-// lost 6-7 % to the int16 rows (four loads and a decode per gift pair)
-#ifndef LB_PREFETCH
-#define LB_PREFETCH 0
-#endif
-#ifndef LB_PACKED
-#define LB_PACKED 0
-#endif
-#ifndef LB_CFG_2048
-#define LB_CFG_2048 0  // 1024 < n <= 2048: 0 = 8 waves x 4 columns, 1 = 4 x 8, 2 = 16 x 2
-#endif
 constexpr int LB_TSH = 12;                 // sbp's step field and the key's tie field
 constexpr int32_t LB_BIAS = 1 << 19;       // spc_V + BIAS in [0, 2^20)
 constexpr int LB_MAX_N = 2048;             // 11-bit positions
