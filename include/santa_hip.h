@@ -152,6 +152,16 @@ void sh_ctx_destroy(sh_ctx *ctx);
 int sh_sample_blocks(uint64_t seed, uint64_t round, int lo, int count, int stride,
                      int n, int B, int32_t *d_rows, void *stream);
 
+/* sh_sample_blocks + the round's undo record in the same launch:
+ *   d_undo[k] = d_types[d_rows[k]]   (the gift types the round starts from)
+ * Blocks are disjoint and a round changes only its blocks' rows (twins and
+ * triplets: the other members carry the first member's type), so
+ * sh_unpack_types(d_types, d_rows, n*B, d_undo, mode) undoes the round --
+ * the rollback of mpi_twins.py:166-169 (keep-if-improved) and of a
+ * speculative round, without a copy of the whole state every round.       */
+int sh_sample_blocks_undo(uint64_t seed, uint64_t round, int lo, int count, int stride, int n, int B,
+                          int32_t *d_rows, const int16_t *d_types, int16_t *d_undo, void *stream);
+
 /* ---------------------------------------------------------------------------
  * Fused block round.  Replaces optimize_block (mpi_single.py:93-102) /
  * optimize_block_twins (mpi_twins.py:93-105) for B disjoint blocks at once

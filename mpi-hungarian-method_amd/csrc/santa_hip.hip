@@ -4265,9 +4265,11 @@ __device__ __forceinline__ void santa_big_block(const SantaArgs &a, const int b)
 // a workgroup per CU loops over the listed blocks (the lattice kernel left
 // them untouched: out of its checked range, or every block under the test
 // flags) and resets the other parity's list counter for the next call.
-template <int MODE, int NW, int K, int FB>
+// (LIST: a separate instantiation, so that each inlines the block once: with
+// both paths in one kernel the block's registers went to scratch)
+template <int MODE, int NW, int K, int FB, bool LIST = false>
 __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
-  if (a.blist) {
+  if constexpr (LIST) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.ovf_reset) *a.ovf_reset = 0;
     const int cnt = *a.bcount;
     for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
@@ -4990,9 +4992,15 @@ __global__ __launch_bounds__(WAVE * SCORE_WAVES) void score_kernel(ScoreArgs a) 
 // ---------------------------------------------------------------------------
 // Sampler and exchange helpers.
 // ---------------------------------------------------------------------------
-__global__ void sample_kernel(ShFeistel f, int lo, int stride, int total, int32_t *rows) {
+// (types / undo: the round's undo record, sh_sample_blocks_undo)
+__global__ void sample_kernel(ShFeistel f, int lo, int stride, int total, int32_t *rows,
+                              const int16_t *types, int16_t *undo) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < total) rows[k] = lo + stride * (int)sh_feistel_perm(f, (uint64_t)k);
+  if (k < total) {
+    const int r = lo + stride * (int)sh_feistel_perm(f, (uint64_t)k);
+    rows[k] = r;
+    if (undo) undo[k] = types[r];
+  }
 }
 
 __global__ void pack_kernel(const int16_t *types, const int32_t *rows, int count, int16_t *out) {
@@ -5283,7 +5291,21 @@ int sh_sample_blocks(uint64_t seed, uint64_t round, int lo, int count, int strid
   const ShFeistel f = sh_feistel_make(seed, round, (uint64_t)count);
   const int total = n * B;
   hipLaunchKernelGGL(sample_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, f,
-                     lo, stride, total, d_rows);
+                     lo, stride, total, d_rows, (const int16_t *)nullptr, (int16_t *)nullptr);
+  HIP_TRY(hipGetLastError());
+  return SH_OK;
+}
+
+int sh_sample_blocks_undo(uint64_t seed, uint64_t round, int lo, int count, int stride, int n, int B,
+                          int32_t *d_rows, const int16_t *d_types, int16_t *d_undo, void *stream) {
+  if (!d_rows || !d_types || !d_undo || n <= 0 || B < 0 || count <= 0 || stride <= 0)
+    return fail(SH_ERR_ARGS, "bad sampler arguments");
+  if ((int64_t)n * B > count) return fail(SH_ERR_ARGS, "B * n exceeds the eligible count");
+  if (B == 0) return SH_OK;
+  const ShFeistel f = sh_feistel_make(seed, round, (uint64_t)count);
+  const int total = n * B;
+  hipLaunchKernelGGL(sample_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, f,
+                     lo, stride, total, d_rows, d_types, d_undo);
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
@@ -5330,13 +5352,15 @@ int launch_big_cfg(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) 
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total));
     attr.set(ctx->device, L.total);
   }
-  // (the fallback launch of santa_lb_kernel, a block list: a workgroup per CU
-  // loops over it)
-  const int grid = a.blist ? std::max(1, std::min(B, ctx->n_cu)) : B;
-  hipLaunchKernelGGL((santa_big_kernel<MODE, NW, K, FB>), dim3(grid), dim3(NW * WAVE), L.total, s, a);
+  hipLaunchKernelGGL((santa_big_kernel<MODE, NW, K, FB>), dim3(B), dim3(NW * WAVE), L.total, s, a);
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }
+
+// The fallback launch of santa_lb_kernel (singles): a workgroup per CU loops
+// over the listed blocks, in the full-round configuration (fewer waves per
+// block: the loop's registers stay out of scratch).
+int launch_big_list(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s);
 
 template <int NW_, int K_, int FB_>
 struct BigCfg {
@@ -5453,10 +5477,7 @@ int launch_santa_lb(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
     f.blist = a.ovf_list;
     f.bcount = a.ovf_cnt;
     f.ovf_reset = ctx->d_ovf + (p ^ 1);
-    rc = with_big_cfg<0>(ctx, a.n, 1, [&](auto c) {
-      using C = decltype(c);
-      return launch_big_cfg<0, C::NW, C::K, C::FB>(ctx, f, B, s);
-    });
+    rc = launch_big_list(ctx, f, B, s);
   }
   if (rc) {
     (void)hipMemsetAsync(ctx->d_ovf + p, 0, sizeof(int32_t), s);
@@ -5464,6 +5485,29 @@ int launch_santa_lb(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   }
   ctx->ovf_par = p ^ 1;
   return SH_OK;
+}
+
+int launch_big_list(const sh_ctx *ctx, const SantaArgs &a, int B, hipStream_t s) {
+  // (with_big_cfg's full-round picks for n <= LB_MAX_N, spelled out so that
+  // only these instantiations exist)
+  auto go = [&](auto c) {
+    using C = decltype(c);
+    const BigLds L = big_lds_layout(a.n, 0, ctx->ng, C::NW, C::K);
+    if (a.n > C::NW * WAVE * C::K || L.total > 160 * 1024) return fail(SH_ERR_ARGS, "large-block fallback: bad config");
+    static thread_local AttrCache attr;
+    if (L.total > 64 * 1024 && attr.need(ctx->device, L.total)) {
+      HIP_TRY(hipFuncSetAttribute((const void *)santa_big_kernel<0, C::NW, C::K, C::FB, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.total));
+      attr.set(ctx->device, L.total);
+    }
+    hipLaunchKernelGGL((santa_big_kernel<0, C::NW, C::K, C::FB, true>), dim3(std::max(1, std::min(B, ctx->n_cu))),
+                       dim3(C::NW * WAVE), L.total, s, a);
+    HIP_TRY(hipGetLastError());
+    return SH_OK;
+  };
+  if (a.n <= 512) return go(BigCfg<2, 4, 10>{});
+  if (a.n <= 1024) return go(BigCfg<4, 4, 10>{});
+  return go(BigCfg<8, 4, 12>{});
 }
 
 template <int MODE>

@@ -85,6 +85,7 @@ SIGNATURES = {
     "sh_ctx_create": (_I, [ctypes.POINTER(_P), _I, _P, _I, _P, _I, _I, _I, _I]),
     "sh_ctx_destroy": (None, [_P]),
     "sh_sample_blocks": (_I, [_U64, _U64, _I, _I, _I, _I, _I, _P, _P]),
+    "sh_sample_blocks_undo": (_I, [_U64, _U64, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "sh_solve_blocks": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _U, _P]),
     "sh_score": (_I, [_P, _P, _P, _P]),
     "sh_ctx_error_flags": (_I, [_P, _P]),

@@ -113,6 +113,24 @@ class SantaGPU:
         _lib.check(rc, "sh_sample_blocks")
         return rows
 
+    def sample_blocks_undo(self, mode: int, n: int, B: int, seed: int, round_: int, types: torch.Tensor,
+                           out: torch.Tensor, undo: torch.Tensor) -> torch.Tensor:
+        """sample_blocks + the round's undo record in one launch: undo[k] =
+        types[rows[k]] (the round's starting types at its rows); unpack_types(
+        types, rows, undo, mode) undoes the round (sh_sample_blocks_undo)."""
+        lo, count, stride, nb = self.geometry(mode, n)
+        if B > nb:
+            raise ValueError(f"only {nb} disjoint blocks of {n} exist, asked for {B}")
+        assert out.dtype == torch.int32 and out.numel() >= B * n and out.device == self.device
+        assert undo.dtype == torch.int16 and undo.numel() >= B * n and undo.device == self.device
+        assert types.dtype == torch.int16 and types.numel() == self.nc and types.device == self.device
+        with torch.cuda.device(self.device):
+            rc = _lib.lib().sh_sample_blocks_undo(ctypes.c_uint64(seed), ctypes.c_uint64(round_), lo, count,
+                                                  stride, n, B, _ptr(out), _ptr(types), _ptr(undo),
+                                                  self.stream)
+        _lib.check(rc, "sh_sample_blocks_undo")
+        return out
+
     # -- A2-A6 fused block round ----------------------------------------------------
     def solve_blocks(self, mode: int, rows: torch.Tensor, n: int, types: torch.Tensor,
                      col: torch.Tensor | None = None, cost: torch.Tensor | None = None,

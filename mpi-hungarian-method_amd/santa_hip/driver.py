@@ -294,10 +294,10 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
         return res
     for rnd in range(max_rounds):
         t0 = time.perf_counter()
-        rows = engine.sample_blocks(mode, n, B, seed, rnd)
+        rows, tok = _sample(engine, mode, n, B, seed, rnd, types)
         if check_disjoint:
             assert_disjoint(rows, mode)
-        if backup is not None:
+        if backup is not None and tok is None:
             backup.copy_(types)
         d = sums.buffer(0) if sums.delta else None
         if b1 > b0:
@@ -309,7 +309,8 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
             check_engine_errors(engine, world, types.device)
         if sums.delta:
             sc, sg, bad_tri, bad_tw = sums.combine(
-                cur, rnd, *engine.delta_begin(types, d, sums.check_round(rnd), after=sums.reduce(d)).result())
+                cur, rnd, *engine.delta_begin(types, d, sums.check_round(rnd), after=sums.reduce(d),
+                                              snapshot=False).result())
         else:
             sc, sg, bad_tri, bad_tw = engine.score_sums(types)
         if bad_tri or bad_tw:
@@ -323,7 +324,10 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
             count += 1
         kept = True
         if accept == "improve" and not improved:
-            types.copy_(backup)
+            if tok is not None:
+                tok.undo(types)  # (the round's undo record: its blocks' starting types)
+            else:
+                types.copy_(backup)
             kept = False
         if kept:
             cur = (sc, sg)
@@ -341,6 +345,17 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
     sums.final_check(types, cur, res.history)
     _drain(engine)
     return res
+
+
+def _sample(engine, mode, n, B, seed, rnd, types):
+    """Round rnd's rows and, from engines with sample_round, its undo record
+    (a token whose undo(types) restores the round's starting types at its
+    rows: the round is undone without a copy of the whole state); (rows,
+    None) from the others, which the loops roll back by copies."""
+    sr = getattr(engine, "sample_round", None)
+    if sr is None:
+        return engine.sample_blocks(mode, n, B, seed, rnd), None
+    return sr(mode, n, B, seed, rnd, types)
 
 
 def _drain(engine) -> None:
@@ -362,16 +377,20 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
     b0, b1, _ = shard_range(B, world.rank, world.size)
     buffers: dict = {}
     improve = accept == "improve"
-    pre = [torch.empty_like(types) for _ in range(2)] if improve else None
+    undo_mode = getattr(engine, "sample_round", None) is not None
+    # rollback targets: each round's undo record (undo_mode), or a copy of its
+    # starting state
+    pre = [torch.empty_like(types) for _ in range(2)] if improve and not undo_mode else None
+    tok = [None, None]
     count = 0
     pending = None  # (round, score handle, start time, pre slot) of the round awaiting its score
     stop = False
     rnd = 0
 
     def launch(r: int, k: int):
-        if improve:
+        if pre is not None:
             pre[k].copy_(types)  # round r's starting state (its rollback target)
-        rows = engine.sample_blocks(mode, n, B, seed, r)
+        rows, tok[k] = _sample(engine, mode, n, B, seed, r, types)
         if check_disjoint:
             assert_disjoint(rows, mode)
         d = sums.buffer(k) if sums.delta else None
@@ -382,8 +401,9 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
                      _next_sampler(engine, mode, n, B, seed, r, max_rounds))
         if check_disjoint:
             check_engine_errors(engine, world, types.device)
-        if sums.delta:
-            return engine.delta_begin(types, d, sums.check_round(r), after=sums.reduce(d))
+        if sums.delta:  # (a snapshot only for a check round's rescore, or for the copy rollback)
+            return engine.delta_begin(types, d, sums.check_round(r), after=sums.reduce(d),
+                                      snapshot=not undo_mode)
         return engine.score_begin(types)
 
     while True:
@@ -410,8 +430,13 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
             else:
                 count += 1
             kept = improved or not improve
-            if not kept:
-                types.copy_(pre[pk])  # the state after round prnd is its starting state
+            if not kept:  # the state after round prnd is its starting state
+                if undo_mode:
+                    if handle is not None:
+                        tok[k].undo(types)  # the speculative round rnd first
+                    tok[pk].undo(types)
+                else:
+                    types.copy_(pre[pk])
             else:
                 cur = (sc, sg)
             res.rounds += 1
@@ -425,7 +450,10 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
             if handle is not None:
                 if stop:  # the serial loop ends after round prnd: undo the speculative round
                     if kept:
-                        ph.restore(types)
+                        if undo_mode:
+                            tok[k].undo(types)
+                        else:
+                            ph.restore(types)
                     handle = None
                 elif not kept:  # round rnd ran from a rejected state: run it again
                     handle = launch(rnd, k)
@@ -530,6 +558,7 @@ class GPUEngine:
         if self._pf_key != key:
             self._pf_key = key
             self._pf_buf = [torch.empty(B * n, dtype=torch.int32, device=self.ctx.device) for _ in range(ring)]
+            self._undo_buf = [torch.empty(B * n, dtype=torch.int16, device=self.ctx.device) for _ in range(ring)]
             self._pf_rnd = [None] * ring
             self._pf_ev = [None] * ring
         return ring, torch.cuda.current_stream(self.ctx.device), rnd % ring
@@ -541,6 +570,31 @@ class GPUEngine:
         if self._pf_rnd[k] != rnd:
             self.ctx.sample_blocks(mode, n, B, seed, rnd, out=self._pf_buf[k])
             self._pf_rnd[k] = rnd
+
+    def sample_round(self, mode, n, B, seed, rnd, types):
+        """Round rnd's rows and its undo record (run_rounds' undo protocol):
+        one launch samples the rows and gathers the round's starting types at
+        them (sh_sample_blocks_undo), or, when the rows were sampled ahead
+        (prefetch_blocks: N > 1, behind the previous round's all-gather and
+        before its unpack), the types are gathered now (sh_pack_types).  The
+        token's undo(types) scatters them back (sh_unpack_types); it stays
+        valid until round rnd + 2 is sampled (a ring of two buffers)."""
+        ring, main, k = self._ring(mode, n, B, seed, rnd)
+        rows, undo, cnt = self._pf_buf[k], self._undo_buf[k], B * n
+        if self._pf_ev[k] is not None:
+            _wait(main, self._pf_ev[k])
+            self._pf_ev[k] = None
+        if self._pf_rnd[k] == rnd:
+            self.ctx.pack_types(types, rows[:cnt], undo[:cnt])
+        else:
+            self.ctx.sample_blocks_undo(mode, n, B, seed, rnd, types, out=rows, undo=undo)
+            self._pf_rnd[k] = rnd
+        ctx = self.ctx
+
+        class _Undo:
+            def undo(_, t):
+                ctx.unpack_types(t, rows[:cnt], undo[:cnt], mode)
+        return rows, _Undo()
 
     def prefetch_blocks(self, mode, n, B, seed, rnd):
         """Sample round rnd's blocks now, on the round's stream, for the next
@@ -594,14 +648,16 @@ class GPUEngine:
         snapshot back (pipelined rounds)."""
         return self._begin(types, None, True)
 
-    def delta_begin(self, types, d, full: bool, after=None):
-        """Delta rounds: snapshot `types`, copy the delta d to the host (once
-        `after`, its all-reduce's work handle, is done) and, if `full`, rescore
-        the snapshot on the side stream; result() -> (dS_child, dS_gift, full
-        sums or None)."""
-        return self._begin(types, d, full, after)
+    def delta_begin(self, types, d, full: bool, after=None, snapshot: bool = True):
+        """Delta rounds: copy the delta d to the host (once `after`, its
+        all-reduce's work handle, is done) and, if `full`, rescore a snapshot
+        of `types` on the side stream; result() -> (dS_child, dS_gift, full
+        sums or None).  snapshot=False (the undo protocol, sample_round): no
+        snapshot unless `full` -- no 2 MB copy on the round's stream -- and
+        the handle cannot restore()."""
+        return self._begin(types, d, full, after, snapshot)
 
-    def _begin(self, types, d, full: bool, after=None):
+    def _begin(self, types, d, full: bool, after=None, snapshot: bool = True):
         if not hasattr(self, "_snaps"):
             dev = types.device
             self._side_stream()
@@ -614,10 +670,11 @@ class GPUEngine:
         k = self._k
         self._k ^= 1
         main = torch.cuda.current_stream(types.device)
-        if self._done[k] is not None:
-            _wait(main, self._done[k])  # the score two rounds back has read the snapshot
         snap = self._snaps[k]
-        snap.copy_(types)
+        if snapshot or full:
+            if self._done[k] is not None:
+                _wait(main, self._done[k])  # the score two rounds back has read the snapshot
+            snap.copy_(types)
         dhost = self._dhost[k]
         side = self._side if self.SIDE_STREAM else main
         # everything after the snapshot runs on the side stream: the delta's
@@ -657,6 +714,8 @@ class GPUEngine:
                 return int(dhost[0]), int(dhost[1]), sums
 
             def restore(_, t):
+                if not (snapshot or full):
+                    raise RuntimeError("no snapshot was taken for this round (undo protocol)")
                 torch.cuda.current_stream(t.device).wait_event(done)
                 t.copy_(snap)
         return _Handle()

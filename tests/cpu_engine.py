@@ -30,6 +30,7 @@ class CPUOracleEngine:
         self.score_log = []  # (S_child, S_gift, types sha) of every scored state
         self.prefetched = []  # rounds passed to prefetch_blocks
         self.drained = 0  # run_rounds' end-of-run drain() calls
+        self.undo_tokens = 0  # rounds sampled with an undo record (sample_round)
 
     def geometry(self, mode, n):
         if mode == _lib.SH_MODE_SINGLE:
@@ -44,6 +45,22 @@ class CPUOracleEngine:
     def sample_blocks(self, mode, n, B, seed, rnd):
         lo, count, stride, _ = self.geometry(mode, n)
         return torch.from_numpy(sample_blocks(seed, rnd, lo, count, stride, n, B).reshape(-1).copy())
+
+    def sample_round(self, mode, n, B, seed, rnd, types):
+        """GPUEngine.sample_round (the undo protocol): the rows and a token
+        whose undo(types) restores the round's starting types at its rows (all
+        members of a unit)."""
+        rows = self.sample_blocks(mode, n, B, seed, rnd)
+        r = rows.numpy()
+        saved = types.numpy()[r].copy()
+        self.undo_tokens += 1
+
+        class _Undo:
+            def undo(_, t):
+                tt = t.numpy()
+                for m in range(mode + 1):
+                    tt[r + m] = saved
+        return rows, _Undo()
 
     def prefetch_blocks(self, mode, n, B, seed, rnd):
         """GPUEngine.prefetch_blocks (the exchange's `during` hook): nothing to
@@ -65,8 +82,9 @@ class CPUOracleEngine:
     def new_delta(self):
         return torch.zeros(2, dtype=torch.int64)
 
-    def delta_begin(self, types, d, full, after=None):
-        """Delta-round protocol (GPUEngine.delta_begin)."""
+    def delta_begin(self, types, d, full, after=None, snapshot=True):
+        """Delta-round protocol (GPUEngine.delta_begin; the host copy is the
+        snapshot whatever `snapshot` says)."""
         if after is not None:
             after.wait()  # (d's all-reduce)
         snap = types.clone()

@@ -160,20 +160,30 @@ def test_pipelined_rounds_equal_serial(mode, n, accept, warm, patience, rounds):
 
 
 def _serial_vs_pipelined(sd, start, mode, n, accept, patience, rounds):
-    """Run both loops from `start`; assert identical state, history and
-    counts; return (rounds run, whether any round was rejected)."""
+    """Run both loops from `start`, each with the undo protocol (rollbacks and
+    the speculative round undone from each round's undo record) and with
+    whole-state copies (an engine without sample_round); assert identical
+    state, history and counts; return (rounds run, whether any round was
+    rejected)."""
     from cpu_engine import CPUOracleEngine
+
+    class Copies(CPUOracleEngine):
+        sample_round = None  # (the loops fall back to snapshots and copies)
+
     out = []
     for pipeline in (False, True):
-        eng = CPUOracleEngine(sd.wish, sd.goodkids, sd.nq)
-        t = start.clone()
-        res = run_rounds(eng, t, mode=mode, n=n, seed=5, max_rounds=rounds, accept=accept,
-                         patience=patience, world=World(), pipeline=pipeline)
-        hist = [(st.round, st.s_child, st.s_gift, st.score, st.accepted, st.best) for st in res.history]
-        out.append((t.numpy().copy(), hist, res.rounds, res.blocks_solved, res.best_score))
-    (t0, h0, r0, b0, s0), (t1, h1, r1, b1, s1) = out
-    assert np.array_equal(t0, t1)
-    assert h0 == h1 and r0 == r1 and b0 == b1 and s0 == s1
+        for cls in (CPUOracleEngine, Copies):
+            eng = cls(sd.wish, sd.goodkids, sd.nq)
+            t = start.clone()
+            res = run_rounds(eng, t, mode=mode, n=n, seed=5, max_rounds=rounds, accept=accept,
+                             patience=patience, world=World(), pipeline=pipeline)
+            assert (eng.undo_tokens > 0) == (cls is CPUOracleEngine and rounds > 0)
+            hist = [(st.round, st.s_child, st.s_gift, st.score, st.accepted, st.best) for st in res.history]
+            out.append((t.numpy().copy(), hist, res.rounds, res.blocks_solved, res.best_score))
+    t0, h0, r0, b0, s0 = out[0]
+    for t1, h1, r1, b1, s1 in out[1:]:
+        assert np.array_equal(t0, t1)
+        assert h0 == h1 and r0 == r1 and b0 == b1 and s0 == s1
     return r0, any(not a for (_, _, _, _, a, _) in h0)
 
 

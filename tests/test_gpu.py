@@ -352,10 +352,10 @@ def test_bench_rounds_vs_oracle(sh, ctx, full_data, mode, pinned, rounds):
             assert dl.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]], k
             checked.append(k)
 
-        def delta_begin(self, t, d, full, after=None):
+        def delta_begin(self, t, d, full, after=None, **kw):
             # the round's post-round state (before a keep-if-improved rollback)
             post.append(oracle.score_sums(full_data.wish, full_data.goodkids, t.cpu().numpy())[:2])
-            return super().delta_begin(t, d, full, after)
+            return super().delta_begin(t, d, full, after, **kw)
 
         def score_sums(self, t):
             s = super().score_sums(t)
