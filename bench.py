@@ -460,15 +460,15 @@ def main():
             self.timed = False
             self.ev = []
 
-        def solve_blocks(self, mode_, rows_, n_, types_, delta=None):
+        def solve_blocks(self, mode_, rows_, n_, types_, delta=None, steps=None):
             if not self.timed:
-                return self.ctx.solve_blocks(mode_, rows_, n_, types_, delta=delta)
+                return super().solve_blocks(mode_, rows_, n_, types_, delta=delta)
             k = len(self.ev)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            self.ctx.solve_blocks(mode_, rows_, n_, types_, delta=delta,
-                                  steps=steps_dev[k] if k < max_calls else None)
+            super().solve_blocks(mode_, rows_, n_, types_, delta=delta,
+                                 steps=steps_dev[k] if k < max_calls else None)
             e1.record(stream)
             self.ev.append((e0, e1))
 

@@ -1172,7 +1172,35 @@ struct SantaArgs {
   const int32_t *blist;   // [*bcount] or null = every block
   const int32_t *bcount;
   int32_t *ovf_reset;
+  // sh_solve_round: this round's undo record (the starting types of its rows)
+  // and the next round's rows, sampled by the launch's workgroups (each a
+  // share); null in sh_solve_blocks and in every fallback launch
+  int16_t *undo;          // [B * n] or null
+  int32_t *nx_rows;       // [nx_total] or null
+  ShFeistel nx_f;
+  int nx_lo, nx_stride, nx_total;
 };
+
+// The round's prologue of every Santa block kernel (sh_solve_round), before
+// the block touches the gift types: its undo record (the starting types of
+// its rows; a unit's other members carry the first member's type) and this
+// workgroup's share of the next round's rows (sh_sample_blocks' values, the
+// grid splitting them) -- the sampling launch between two rounds' kernels
+// is gone.
+__device__ __forceinline__ void round_prologue(const SantaArgs &a, const int b, const int mode) {
+  if (a.undo) {
+    for (int j = (int)threadIdx.x; j < a.n; j += (int)blockDim.x) {
+      const int r = a.rows[(size_t)b * a.n + j];
+      if (r >= 0 && r + mode < a.nc) a.undo[(size_t)b * a.n + j] = a.types[r];
+    }
+  }
+  if (a.nx_rows) {
+    const int per = (a.nx_total + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int k0 = (int)blockIdx.x * per, k1 = min(a.nx_total, k0 + per);
+    for (int k = k0 + (int)threadIdx.x; k < k1; k += (int)blockDim.x)
+      a.nx_rows[k] = a.nx_lo + a.nx_stride * (int)sh_feistel_perm(a.nx_f, (uint64_t)k);
+  }
+}
 
 __device__ __forceinline__ int64_t gift_happy(const SantaArgs &a, int child, int t) {
   const int e0 = a.csr_off[child], e1 = a.csr_off[child + 1];
@@ -1449,6 +1477,7 @@ __device__ __forceinline__ bool fast_tile_build(const SantaArgs &a, const int b,
 
 template <int K, int MODE, bool TIMED = false>
 __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
+  round_prologue(a, blockIdx.x, MODE);
   static_assert(K == 1, "one column per thread (n <= 256)");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
@@ -2002,6 +2031,7 @@ __global__ __launch_bounds__(VT_WG, SV == 0 ? 1 : 4) void santa_vt_kernel(SantaA
       __syncthreads();  // (LDS reused by the next listed block)
     }
   } else {
+    round_prologue(a, blockIdx.x, MODE);
     santa_vt_block<MODE, SV>(a, blockIdx.x);
   }
 }
@@ -2083,6 +2113,7 @@ __device__ __forceinline__ uint64_t rfl_u64(uint64_t x) {
 
 template <bool VEC>
 __global__ __launch_bounds__(WAVE, 2) void santa_sp_kernel(SantaArgs a) {
+  round_prologue(a, blockIdx.x, 0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
@@ -2670,6 +2701,7 @@ __host__ __device__ __forceinline__ TileLds tile_lds_layout(int ng) {
 // loads touching one line.
 template <int LV>
 __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(4))) void santa_tile_kernel(SantaArgs a, unsigned char *rec_all) {
+  round_prologue(a, blockIdx.x, 0);
   constexpr bool VEC = LV != 0;  // (n_wish % 4 == 0: no per-gift bound test)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
@@ -3036,6 +3068,7 @@ struct Sp3LdsFused {
 
 template <bool TIMED, bool FUSED>
 __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const unsigned char *rec_all) {
+  if constexpr (FUSED) round_prologue(a, blockIdx.x, 0);  // (else santa_tile_kernel ran it)
   using SL = std::conditional_t<FUSED, Sp3LdsFused, Sp3LdsRecord>;
   __shared__ __attribute__((aligned(16))) SL SM;
   int32_t *rowc, *u_l;
@@ -3723,6 +3756,7 @@ __host__ __device__ __forceinline__ DtLds dt_lds_layout(int n, int ng) {
 }
 
 __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
+  round_prologue(a, blockIdx.x, 0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -4277,6 +4311,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_big_kernel(SantaArgs a) {
       __syncthreads();  // (LDS reused by the next listed block)
     }
   } else {
+    round_prologue(a, blockIdx.x, MODE);
     santa_big_block<MODE, NW, K, FB>(a, blockIdx.x);
   }
 }
@@ -4382,6 +4417,7 @@ struct LbRange {
 //           (the winner leaves `remaining`, the mover's tie bits) in their shadow
 template <int NW, int K, bool TIMED = false>
 __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
+  round_prologue(a, blockIdx.x, 0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int WG = NW * WAVE;
   constexpr int NCOL = WG * K;
@@ -5477,6 +5513,10 @@ int launch_santa_lb(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
     f.blist = a.ovf_list;
     f.bcount = a.ovf_cnt;
     f.ovf_reset = ctx->d_ovf + (p ^ 1);
+    f.undo = nullptr;
+    f.nx_rows = nullptr;
+  f.undo = nullptr;
+  f.nx_rows = nullptr;
     rc = launch_big_list(ctx, f, B, s);
   }
   if (rc) {
@@ -5534,6 +5574,10 @@ int launch_santa_vt_sc(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
     f.blist = a.ovf_list;
     f.bcount = a.ovf_cnt;
     f.ovf_reset = ctx->d_ovf + (p ^ 1);
+    f.undo = nullptr;
+    f.nx_rows = nullptr;
+  f.undo = nullptr;
+  f.nx_rows = nullptr;
     rc = launch_santa_vt<0, 0>(ctx, f, B, s);
   }
   if (rc) {
@@ -5571,6 +5615,8 @@ int launch_santa_dt(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   f.blist = a.ovf_list;
   f.bcount = a.ovf_cnt;
   f.ovf_reset = ctx->d_ovf + (p ^ 1);
+  f.undo = nullptr;
+  f.nx_rows = nullptr;
   const int rc = launch_santa_vt<0, 0>(ctx, f, B, s);
   if (rc) {
     (void)hipMemsetAsync(ctx->d_ovf + p, 0, sizeof(int32_t), s);
@@ -5635,6 +5681,8 @@ int launch_santa_sp(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s, bool tile2) 
   f.blist = a.ovf_list;
   f.bcount = a.ovf_cnt;
   f.ovf_reset = ctx->d_ovf + (p ^ 1);
+  f.undo = nullptr;
+  f.nx_rows = nullptr;
   const int rc = launch_santa_vt<0>(ctx, f, B, s);
   if (rc) {
     // the sparse launch may have appended to counter p: clear it so that a
@@ -5786,7 +5834,17 @@ extern "C" {
 int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, int16_t *d_types,
                     int32_t *d_col, int64_t *d_cost, int64_t *d_delta, int64_t *d_steps,
                     unsigned flags, void *stream) {
+  return sh_solve_round(ctx, mode, d_rows, n, B, d_types, d_col, d_cost, d_delta, d_steps, nullptr, nullptr,
+                        flags, stream);
+}
+
+int sh_solve_round(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, int16_t *d_types,
+                   int32_t *d_col, int64_t *d_cost, int64_t *d_delta, int64_t *d_steps, int16_t *d_undo,
+                   const sh_next_rows *next, unsigned flags, void *stream) {
   if (!ctx || (!d_rows && B > 0) || !d_types) return fail(SH_ERR_ARGS, "null pointer");
+  if (next && (!next->d_rows || next->B < 0 || next->count <= 0 || next->stride <= 0 ||
+               (int64_t)n * next->B > next->count))
+    return fail(SH_ERR_ARGS, "bad next-round sampler arguments");
   if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS && mode != SH_MODE_TRIPLETS)
     return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA) return fail(SH_ERR_ARGS, "n must be in [1, 4096]");
@@ -5802,6 +5860,17 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, 
   a.n_wish = ctx->n_wish; a.n_good = ctx->n_good; a.flags = flags;
   a.cap = 0; a.ovf_cnt = nullptr; a.ovf_list = nullptr;
   a.blist = nullptr; a.bcount = nullptr; a.ovf_reset = nullptr;
+  a.undo = d_undo;
+  a.nx_rows = nullptr;
+  a.nx_lo = a.nx_stride = a.nx_total = 0;
+  a.nx_f = ShFeistel{};
+  if (next && next->B > 0) {
+    a.nx_rows = next->d_rows;
+    a.nx_f = sh_feistel_make(next->seed, next->round, (uint64_t)next->count);
+    a.nx_lo = next->lo;
+    a.nx_stride = next->stride;
+    a.nx_total = n * next->B;
+  }
   hipStream_t s = (hipStream_t)stream;
   switch (pick_design(ctx, mode, n, B, flags)) {
     case SH_DESIGN_LARGE:

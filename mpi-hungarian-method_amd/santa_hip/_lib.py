@@ -87,6 +87,7 @@ SIGNATURES = {
     "sh_sample_blocks": (_I, [_U64, _U64, _I, _I, _I, _I, _I, _P, _P]),
     "sh_sample_blocks_undo": (_I, [_U64, _U64, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "sh_solve_blocks": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _U, _P]),
+    "sh_solve_round": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _U, _P]),
     "sh_score": (_I, [_P, _P, _P, _P]),
     "sh_ctx_error_flags": (_I, [_P, _P]),
     "sh_ctx_fallback_steps": (_I, [_P, _P]),
@@ -101,6 +102,13 @@ SIGNATURES = {
     "lsap_solve_batched_hash": (_I, [_U64, _I64, _I, _I, _P, _P, _U, _P]),
     "sh_gen_synthetic": (_I, [_U64, _I, _I, _I, _I, _I, _P, _P, _P]),
 }
+
+
+class NextRows(ctypes.Structure):
+    """sh_next_rows (include/santa_hip.h): the next round's sampler arguments."""
+    _fields_ = [("seed", ctypes.c_uint64), ("round", ctypes.c_uint64), ("lo", ctypes.c_int),
+                ("count", ctypes.c_int), ("stride", ctypes.c_int), ("B", ctypes.c_int),
+                ("d_rows", ctypes.c_void_p)]
 
 
 class SantaHipError(RuntimeError):

@@ -151,6 +151,37 @@ class SantaGPU:
                                         _lib.SH_COMPAT_TIEBREAK | flags, self.stream)
         _lib.check(rc, "sh_solve_blocks")
 
+    def solve_round(self, mode: int, rows: torch.Tensor, n: int, types: torch.Tensor,
+                    undo: torch.Tensor | None = None, next_round: tuple | None = None,
+                    col: torch.Tensor | None = None, cost: torch.Tensor | None = None,
+                    delta: torch.Tensor | None = None, steps: torch.Tensor | None = None,
+                    flags: int = 0) -> None:
+        """solve_blocks + the loop's round bookkeeping in the same launch
+        (sh_solve_round): undo[k] = the round's starting type at rows[k], and
+        next_round = (seed, round, B, out) samples that round's rows into out
+        (the values sample_blocks writes)."""
+        assert rows.dtype == torch.int32 and rows.is_contiguous() and rows.device == self.device
+        assert types.dtype == torch.int16 and types.numel() == self.nc and types.device == self.device
+        B = rows.numel() // n
+        assert B * n == rows.numel()
+        for t, dt, size in ((col, torch.int32, B * n), (cost, torch.int64, B), (delta, torch.int64, 2),
+                            (steps, torch.int64, B), (undo, torch.int16, B * n)):
+            if t is not None:
+                assert t.dtype == dt and t.numel() >= size and t.device == self.device
+        nx = None
+        if next_round is not None:
+            seed, rnd, Bn, out = next_round
+            lo, count, stride, nb = self.geometry(mode, n)
+            if Bn > nb:
+                raise ValueError(f"only {nb} disjoint blocks of {n} exist, asked for {Bn}")
+            assert out.dtype == torch.int32 and out.numel() >= Bn * n and out.device == self.device
+            nx = _lib.NextRows(seed, rnd, lo, count, stride, Bn, out.data_ptr())
+        rc = _lib.lib().sh_solve_round(self._h, mode, _ptr(rows), n, B, _ptr(types), _ptr(col), _ptr(cost),
+                                       _ptr(delta), _ptr(steps), _ptr(undo),
+                                       ctypes.byref(nx) if nx is not None else None,
+                                       _lib.SH_COMPAT_TIEBREAK | flags, self.stream)
+        _lib.check(rc, "sh_solve_round")
+
     def solve_design(self, mode: int, n: int, B: int, flags: int = 0) -> int:
         """The kernel design (SH_DESIGN_*) solve_blocks dispatches to."""
         rc = _lib.lib().sh_solve_design(self._h, mode, n, B, _lib.SH_COMPAT_TIEBREAK | flags)

@@ -272,6 +272,9 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
                          "raises IndexError at mpi_twins.py:132)")
     res = LoopResult()
     sums = _Sums(engine, world, score_check_every, max_rounds)
+    budget = getattr(engine, "set_round_budget", None)
+    if budget is not None:
+        budget(max_rounds)
     if getattr(engine, "error_flags", None) is not None:
         engine.error_flags()  # the flags cover this run only: drop what earlier calls left
     if sums0 is None and (score0 is None or sums.delta):
@@ -507,6 +510,8 @@ class GPUEngine:
         self.ctx = ctx
         self._pf_key = None
         self._zero_ev = {}
+        self._cur = None     # (slot, round, mode, n, B, seed) of the round sample_round returned last
+        self._budget = None  # rounds the loop runs (set_round_budget): no next-round sampling after the last
 
     def geometry(self, mode, n):
         return self.ctx.geometry(mode, n)
@@ -523,6 +528,15 @@ class GPUEngine:
     # (profiles/r04_gap_probe.json: loop_p0_* against loop_p2_*)
     PREFETCH = 0
     SIDE_STREAM = True  # the round's bookkeeping after the snapshot on the side stream
+    # round r's block kernel samples round r + 1's rows (sh_solve_round) when
+    # it solves the whole round (one GPU): a ring of three row buffers keeps
+    # rounds r - 1 (a pending rollback), r and r + 1 apart
+    FUSED_SAMPLING = True
+    RING = 3
+
+    def set_round_budget(self, max_rounds):
+        """run_rounds' round budget: the last round samples no successor."""
+        self._budget = max_rounds
 
     def sample_blocks(self, mode, n, B, seed, rnd):
         """Round rnd's block rows (A1): sampled on the round's stream (or
@@ -554,13 +568,14 @@ class GPUEngine:
 
     def _ring(self, mode, n, B, seed, rnd):
         key = (mode, n, B, seed)
-        ring = max(self.PREFETCH + 1, 2)
+        ring = max(self.PREFETCH + 1, self.RING)
         if self._pf_key != key:
             self._pf_key = key
             self._pf_buf = [torch.empty(B * n, dtype=torch.int32, device=self.ctx.device) for _ in range(ring)]
             self._undo_buf = [torch.empty(B * n, dtype=torch.int16, device=self.ctx.device) for _ in range(ring)]
             self._pf_rnd = [None] * ring
             self._pf_ev = [None] * ring
+            self._by_solve = [False] * ring  # rows sampled by the previous round's block kernel
         return ring, torch.cuda.current_stream(self.ctx.device), rnd % ring
 
     def _sample_into(self, mode, n, B, seed, rnd, main, k):
@@ -570,6 +585,7 @@ class GPUEngine:
         if self._pf_rnd[k] != rnd:
             self.ctx.sample_blocks(mode, n, B, seed, rnd, out=self._pf_buf[k])
             self._pf_rnd[k] = rnd
+            self._by_solve[k] = False
 
     def sample_round(self, mode, n, B, seed, rnd, types):
         """Round rnd's rows and its undo record (run_rounds' undo protocol):
@@ -584,11 +600,16 @@ class GPUEngine:
         if self._pf_ev[k] is not None:
             _wait(main, self._pf_ev[k])
             self._pf_ev[k] = None
+        # the undo record is gathered by this round's block kernels when they
+        # solve the whole round (solve_blocks), else here
+        self._cur = (k, rnd, mode, n, B, seed, self._pf_rnd[k] == rnd and self._by_solve[k])
         if self._pf_rnd[k] == rnd:
-            self.ctx.pack_types(types, rows[:cnt], undo[:cnt])
+            if not self._cur[6]:
+                self.ctx.pack_types(types, rows[:cnt], undo[:cnt])
         else:
             self.ctx.sample_blocks_undo(mode, n, B, seed, rnd, types, out=rows, undo=undo)
             self._pf_rnd[k] = rnd
+            self._by_solve[k] = False
         ctx = self.ctx
 
         class _Undo:
@@ -615,8 +636,31 @@ class GPUEngine:
             _wait(torch.cuda.current_stream(d.device), ev)
         return d
 
-    def solve_blocks(self, mode, rows, n, types, delta=None):
-        self.ctx.solve_blocks(mode, rows, n, types, delta=delta)
+    def solve_blocks(self, mode, rows, n, types, delta=None, steps=None):
+        """The round's blocks (or this rank's shard).  When the round came
+        from sample_round and this call solves all of it (one GPU), the block
+        kernels also write the round's undo record, if sample_round left it to
+        them, and sample the next round's rows (sh_solve_round)."""
+        cur = self._cur
+        self._cur = None
+        full = (cur is not None and self.FUSED_SAMPLING and rows.numel() == cur[4] * n
+                and rows.data_ptr() == self._pf_buf[cur[0]].data_ptr())
+        if not full:
+            if cur is not None and cur[6]:  # (the undo record was left to the kernels: gather it now)
+                k = cur[0]
+                self.ctx.pack_types(types, self._pf_buf[k][:cur[4] * n], self._undo_buf[k][:cur[4] * n])
+            self.ctx.solve_blocks(mode, rows, n, types, delta=delta, steps=steps)
+            return
+        k, rnd, mode_, n_, B, seed, undo_pending = cur
+        nxt = None
+        if self._budget is None or rnd + 1 < self._budget:
+            k1 = (rnd + 1) % len(self._pf_buf)
+            if self._pf_rnd[k1] != rnd + 1 and self._pf_ev[k1] is None:
+                nxt = (seed, rnd + 1, B, self._pf_buf[k1])
+                self._pf_rnd[k1] = rnd + 1
+                self._by_solve[k1] = True
+        self.ctx.solve_round(mode, rows, n, types, undo=self._undo_buf[k] if undo_pending else None,
+                             next_round=nxt, delta=delta, steps=steps)
 
     def new_delta(self):
         return torch.zeros(2, dtype=torch.int64, device=self.ctx.device)

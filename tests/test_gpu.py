@@ -1114,3 +1114,38 @@ def test_dense_tile_build_declines_to_the_chains(sh, ctx, full_data, mode, fl):
     assert np.array_equal(cost.cpu().numpy(), ocost)
     assert np.array_equal(types.cpu().numpy(), t_host)
     assert ctx.error_flags() == 0
+
+
+@pytest.mark.parametrize("mode,n,B,fl", [(0, 256, 3730, 0), (0, 256, 466, 0), (0, 256, 64, 32), (0, 256, 64, 8),
+                                         (0, 256, 64, 256), (0, 256, 64, 512), (1, 256, 78, 0), (0, 2000, 24, 0),
+                                         (0, 600, 8, 8192), (2, 256, 6, 0)])
+def test_solve_round_bookkeeping(sh, ctx, full_data, mode, n, B, fl):
+    """sh_solve_round (every design, its fallback launch too: SH_FLAG_TEST_RANGE):
+    the same solve as sh_solve_blocks, the round's undo record equals the
+    starting types at its rows (and scattering it back undoes the round), and
+    the next round's rows equal sh_sample_blocks' for that round."""
+    _, _, _, nb = ctx.geometry(mode, n)
+    rows = ctx.sample_blocks(mode, n, B, 77, 3)
+    outs = []
+    for fused in (False, True):
+        types = ctx.upload_types(full_data.types)
+        col = torch.empty(B * n, dtype=torch.int32, device="cuda")
+        cost = torch.empty(B, dtype=torch.int64, device="cuda")
+        delta = torch.zeros(2, dtype=torch.int64, device="cuda")
+        if fused:
+            undo = torch.full((B * n,), -7, dtype=torch.int16, device="cuda")
+            nxt = torch.full((nb * n,), -1, dtype=torch.int32, device="cuda")
+            ctx.solve_round(mode, rows, n, types, undo=undo, next_round=(77, 4, nb, nxt), col=col, cost=cost,
+                            delta=delta, flags=fl)
+        else:
+            ctx.solve_blocks(mode, rows, n, types, col=col, cost=cost, delta=delta, flags=fl)
+        assert ctx.error_flags() == 0
+        outs.append([x.cpu().numpy() for x in (col, cost, delta, types)])
+    for x, y in zip(*outs):
+        assert np.array_equal(x, y)
+    r = rows.cpu().numpy()
+    assert np.array_equal(undo.cpu().numpy(), full_data.types[r])
+    assert np.array_equal(nxt.cpu().numpy(), ctx.sample_blocks(mode, n, nb, 77, 4).cpu().numpy())
+    types = torch.from_numpy(outs[1][3]).cuda()
+    ctx.unpack_types(types, rows, undo, mode)
+    assert np.array_equal(types.cpu().numpy(), full_data.types)

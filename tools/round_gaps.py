@@ -8,8 +8,14 @@ kernel to the start of the next; gaps > 200 us, outside the round loop,
 dropped) and the kernels of one median gap (name, stream, duration in us)."""
 import csv
 import json
+import re
 import statistics
 import sys
+
+
+def short(name: str) -> str:
+    name = re.sub(r"^void ", "", name).replace("(anonymous namespace)::", "")
+    return name.split("(")[0][:48]
 
 
 def main():
@@ -27,7 +33,7 @@ def main():
     for a, b in zip(mains, mains[1:]):
         g = (b[0] - a[1]) / 1e3
         if 0 <= g <= 200:
-            between = [(x[2].split("(")[0][:48], x[3], round((x[1] - x[0]) / 1e3, 1)) for x in ev
+            between = [(short(x[2]), x[3], round((x[1] - x[0]) / 1e3, 1)) for x in ev
                        if x[0] >= a[1] and x[1] <= b[0]]
             gaps.append((g, between))
     gaps.sort(key=lambda t: t[0])
