@@ -236,6 +236,17 @@ int sh_score(sh_ctx *ctx, const int16_t *d_types, int64_t *d_sums, void *stream)
 #define SH_ERRF_TYPE 4u       /* a block's current gift type outside [0, ng) */
 int sh_ctx_error_flags(sh_ctx *ctx, void *stream);
 
+/* The context's host mailbox: 8 int64 of coherent, device-mapped pinned host
+ * memory.  sh_publish_delta(ctx, d_delta, slot, seq, stream) enqueues one
+ * one-lane kernel that writes d_delta[0..1] into words 4 slot + 1, + 2 and
+ * then seq into word 4 slot (system-scope release), and zeroes d_delta: the
+ * round loop reads a round's delta sums (mpi_single.py:157's score, from the
+ * block kernels' exact deltas) by polling the mailbox for seq -- no device
+ * to host copy, no event and no second stream between two rounds' kernels.
+ * slot in {0, 1}.                                                          */
+int64_t *sh_ctx_mailbox(sh_ctx *ctx);
+int sh_publish_delta(sh_ctx *ctx, int64_t *d_delta, int slot, int64_t seq, void *stream);
+
 /* Tuning / test hook of the default singles kernel: LDS bytes per block
  * (0 = default 20 KiB, i.e. 8 blocks per CU).  The per-row hit lists must fit
  * in what is left after the fixed per-block state; blocks that do not fit

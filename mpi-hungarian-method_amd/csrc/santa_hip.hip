@@ -5039,6 +5039,21 @@ __global__ void sample_kernel(ShFeistel f, int lo, int stride, int total, int32_
   }
 }
 
+// sh_publish_delta: the round's delta sums into the context's host mailbox
+// (coherent mapped host memory), the sequence number last (system-scope
+// release: the host sees it only with the values), then the delta zeroed for
+// its next round.  One lane; vector stores.
+__global__ void publish_kernel(int64_t *d, int64_t *mail, int64_t seq) {
+  if (threadIdx.x == 0) {
+    const int64_t v0 = d[0], v1 = d[1];
+    __hip_atomic_store(mail + 1, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(mail + 2, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(mail, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    d[0] = 0;
+    d[1] = 0;
+  }
+}
+
 __global__ void pack_kernel(const int16_t *types, const int32_t *rows, int count, int16_t *out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < count) {
@@ -5144,6 +5159,8 @@ struct sh_ctx {
   int lds_slots = 0, lds_slots_n = -1;  // cached lds_tile_slots for one n
   int dt_slots = 0, dt_slots_n = -1;    // cached dt_tile_slots for one n
   int vt_slots = -1;                     // cached vt_tile_slots
+  int64_t *h_mail = nullptr;             // host mailbox (sh_publish_delta): coherent, mapped
+  int64_t *d_mail = nullptr;             // its device address
 };
 
 namespace {
@@ -5284,6 +5301,11 @@ int sh_ctx_create(sh_ctx **out, int device, const int16_t *h_wish, int n_wish,
   ctx->max_lds = lds;
   if ((e = hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
     return cleanup(fail(SH_ERR_HIP, hipGetErrorString(e)));
+  if ((e = hipHostMalloc((void **)&ctx->h_mail, 8 * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent)) !=
+          hipSuccess ||
+      (e = hipHostGetDevicePointer((void **)&ctx->d_mail, ctx->h_mail, 0)) != hipSuccess)
+    return cleanup(fail(SH_ERR_HIP, std::string("mailbox: ") + hipGetErrorString(e)));
+  for (int q = 0; q < 8; ++q) ctx->h_mail[q] = 0;
   *out = ctx;
   return SH_OK;
 }
@@ -5298,6 +5320,7 @@ void sh_ctx_destroy(sh_ctx *ctx) {
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   if (ctx->d_ovf) (void)hipFree(ctx->d_ovf);
   if (ctx->d_rec) (void)hipFree(ctx->d_rec);
+  if (ctx->h_mail) (void)hipHostFree(ctx->h_mail);
   delete ctx;
 }
 
@@ -5932,6 +5955,17 @@ int sh_score(sh_ctx *ctx, const int16_t *d_types, int64_t *d_sums, void *stream)
   const int chunks = (ctx->nc + WAVE - 1) / WAVE;
   const int grid = std::min((chunks + SCORE_WAVES - 1) / SCORE_WAVES, 2048);
   hipLaunchKernelGGL(score_kernel, dim3(grid), dim3(WAVE * SCORE_WAVES), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  return SH_OK;
+}
+
+int64_t *sh_ctx_mailbox(sh_ctx *ctx) { return ctx ? ctx->h_mail : nullptr; }
+
+int sh_publish_delta(sh_ctx *ctx, int64_t *d_delta, int slot, int64_t seq, void *stream) {
+  if (!ctx || !d_delta || slot < 0 || slot > 1) return fail(SH_ERR_ARGS, "bad mailbox arguments");
+  DeviceGuard dg(ctx->device);
+  hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_delta, ctx->d_mail + 4 * slot,
+                     seq);
   HIP_TRY(hipGetLastError());
   return SH_OK;
 }

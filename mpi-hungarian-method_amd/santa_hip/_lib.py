@@ -90,6 +90,8 @@ SIGNATURES = {
     "sh_solve_round": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _U, _P]),
     "sh_score": (_I, [_P, _P, _P, _P]),
     "sh_ctx_error_flags": (_I, [_P, _P]),
+    "sh_ctx_mailbox": (ctypes.POINTER(ctypes.c_int64), [_P]),
+    "sh_publish_delta": (_I, [_P, _P, _I, _I64, _P]),
     "sh_ctx_fallback_steps": (_I, [_P, _P]),
     "sh_solve_design": (_I, [_P, _I, _I, _I, _U]),
     "sh_resident_blocks": (_I, [_P, _I, _I, _I, _U]),

@@ -192,6 +192,22 @@ class SantaGPU:
         rc = _lib.lib().sh_resident_blocks(self._h, mode, n, B, _lib.SH_COMPAT_TIEBREAK | flags)
         return _lib.check(rc, "sh_resident_blocks")
 
+    @property
+    def mailbox(self):
+        """The context's host mailbox (8 int64, read live: ctypes array over
+        the coherent pinned words sh_publish_delta writes)."""
+        if getattr(self, "_mail", None) is None:
+            p = _lib.lib().sh_ctx_mailbox(self._h)
+            self._mail = ctypes.cast(p, ctypes.POINTER(ctypes.c_int64 * 8)).contents
+        return self._mail
+
+    def publish_delta(self, delta: torch.Tensor, slot: int, seq: int) -> None:
+        """Enqueue: delta[0..1] -> mailbox words 4 slot + 1, + 2, then seq ->
+        word 4 slot; delta zeroed (sh_publish_delta)."""
+        assert delta.dtype == torch.int64 and delta.numel() >= 2 and delta.device == self.device
+        _lib.check(_lib.lib().sh_publish_delta(self._h, _ptr(delta), int(slot), int(seq), self.stream),
+                   "sh_publish_delta")
+
     def error_flags(self) -> int:
         return _lib.check(_lib.lib().sh_ctx_error_flags(self._h, self.stream), "sh_ctx_error_flags")
 

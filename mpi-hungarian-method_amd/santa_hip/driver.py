@@ -487,6 +487,9 @@ def assert_disjoint(rows: torch.Tensor, mode: int) -> None:
         raise AssertionError("blocks of a round are not disjoint (the in-place apply needs a partition)")
 
 
+_ZEROED = object()  # GPUEngine._zero_ev: the delta was zeroed on the round's stream
+
+
 def _wait(stream, ev) -> None:
     """stream waits for ev, unless ev has completed already (then a wait
     would only add a barrier packet between two block kernels)."""
@@ -628,11 +631,12 @@ class GPUEngine:
 
     def zeroed_delta(self, d):
         """d, zeroed: by the side stream after its previous round's host copy
-        (delta_begin), or here on the current stream the first time."""
+        (delta_begin), by its publish kernel on the round's stream (the
+        mailbox), or here on the current stream the first time."""
         ev = self._zero_ev.pop(d.data_ptr(), None)
         if ev is None:
             d.zero_()
-        else:
+        elif ev is not _ZEROED:
             _wait(torch.cuda.current_stream(d.device), ev)
         return d
 
@@ -701,7 +705,38 @@ class GPUEngine:
         the handle cannot restore()."""
         return self._begin(types, d, full, after, snapshot)
 
+    # one GPU, a round with neither rescore nor snapshot: its delta sums reach
+    # the host through the context's mailbox (one one-lane kernel after the
+    # round's kernels, polled by the host) instead of an event, a second
+    # stream's copy and a cross-stream wait between two rounds' kernels
+    MAILBOX = True
+
+    def _publish(self, d):
+        ctx = self.ctx
+        slot = getattr(self, "_mslot", 0)
+        self._mslot = slot ^ 1
+        seq = getattr(ctx, "_mail_seq", 0) + 1  # (per context: unique across engines)
+        ctx._mail_seq = seq
+        ctx.publish_delta(d, slot, seq)
+        self._zero_ev[d.data_ptr()] = _ZEROED  # (zeroed by the publish kernel, in stream order)
+        mail = ctx.mailbox
+
+        class _Handle:
+            def result(_):
+                spins = 0
+                while mail[4 * slot] != seq:
+                    spins += 1
+                    if spins > 256:
+                        time.sleep(20e-6)
+                return int(mail[4 * slot + 1]), int(mail[4 * slot + 2]), None
+
+            def restore(_, t):
+                raise RuntimeError("no snapshot was taken for this round (undo protocol)")
+        return _Handle()
+
     def _begin(self, types, d, full: bool, after=None, snapshot: bool = True):
+        if self.MAILBOX and d is not None and after is None and not (full or snapshot):
+            return self._publish(d)
         if not hasattr(self, "_snaps"):
             dev = types.device
             self._side_stream()

@@ -1149,3 +1149,22 @@ def test_solve_round_bookkeeping(sh, ctx, full_data, mode, n, B, fl):
     types = torch.from_numpy(outs[1][3]).cuda()
     ctx.unpack_types(types, rows, undo, mode)
     assert np.array_equal(types.cpu().numpy(), full_data.types)
+
+
+def test_publish_delta_mailbox(sh, ctx):
+    """sh_publish_delta: the delta sums reach the host mailbox behind their
+    sequence number (values first, seq last) and the device delta is zeroed
+    for its next round; both slots, sequence numbers that repeat a slot's
+    previous value are never mistaken for new ones (the engine's are per
+    context and increasing)."""
+    mail = ctx.mailbox
+    d = torch.tensor([123456789012, -987654321], dtype=torch.int64, device="cuda")
+    for slot, seq in ((0, 1001), (1, 1002), (0, 1003)):
+        d[0] += slot
+        want = d.cpu().tolist()
+        ctx.publish_delta(d, slot, seq)
+        torch.cuda.synchronize()
+        assert mail[4 * slot] == seq
+        assert [mail[4 * slot + 1], mail[4 * slot + 2]] == want
+        assert d.cpu().tolist() == [0, 0]
+        d.copy_(torch.tensor(want, dtype=torch.int64))

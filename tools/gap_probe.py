@@ -96,12 +96,14 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) * 1e3 / R
 
-    def loop(prefetch=GPUEngine.PREFETCH, side=True):
+    def loop(prefetch=GPUEngine.PREFETCH, side=True, mailbox=True, fused=True):
         types.copy_(base)
 
         class Eng(GPUEngine):
             PREFETCH = prefetch
             SIDE_STREAM = side
+            MAILBOX = mailbox
+            FUSED_SAMPLING = fused
         eng = Eng(ctx)
         s = ctx.score_sums(types)
         torch.cuda.synchronize()
@@ -117,7 +119,10 @@ def main():
                 "sync_sample_main": lambda: run("sync", main_sample=True),
                 "loop_p2_side": lambda: loop(2, True), "loop_p0_main": lambda: loop(0, False),
                 "loop_p0_side": lambda: loop(0, True), "loop_p2_main": lambda: loop(2, False),
-                "loop_p1_side": lambda: loop(1, True)}
+                "loop_p1_side": lambda: loop(1, True),
+                "loop_r5": lambda: loop(0, True, True, True), "loop_r5_nomail": lambda: loop(0, True, False, True),
+                "loop_r5_nofuse": lambda: loop(0, True, True, False),
+                "loop_r5_neither": lambda: loop(0, True, False, False)}
     if args.only:
         variants = {k: v for k, v in variants.items() if k in args.only.split(",")}
     for rep in range(args.reps + 1):
