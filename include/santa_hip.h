@@ -187,23 +187,32 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B,
                     int64_t *d_delta, int64_t *d_steps, unsigned flags, void *stream);
 
 /* sh_solve_blocks + the round bookkeeping of the driver's loop in the same
- * launch (each block kernel's prologue, before it touches the gift types):
- *   d_undo  int16 [B x n] (nullable)  the round's undo record,
- *           d_undo[k] = d_types[d_rows[k]] (see sh_sample_blocks_undo)
- *   next    (nullable)  the next round's rows, sampled by the launch's
- *           workgroups: next->d_rows[k] = the value sh_sample_blocks(
- *           next->seed, next->round, next->lo, next->count, next->stride, n,
- *           next->B) writes -- so no sampling launch runs between two rounds'
- *           block kernels (one GPU holding the whole round).
+ * launches (ext nullable; every field optional):
+ *   d_undo  int16 [B x n]  the round's undo record, d_undo[k] =
+ *           d_types[d_rows[k]] before the round (see sh_sample_blocks_undo),
+ *           written by each block kernel's prologue before it touches the types
+ *   next_*  the next round's rows, sampled by the launch's workgroups:
+ *           next_rows[k] = the value sh_sample_blocks(next_seed, next_round,
+ *           next_lo, next_count, next_stride, n, next_B) writes -- so no
+ *           sampling launch runs between two rounds' block kernels
+ *           (next_rows NULL or next_B = 0: no sampling)
+ *   publish the round's delta sums into mailbox slot publish_slot with
+ *           sequence number publish_seq, d_delta zeroed after (exactly
+ *           sh_publish_delta after the round; d_delta required).  Designs
+ *           whose last launch is the fallback register-tile launch fold it
+ *           into that launch's last workgroup.
  * The fallback launches of a design neither record nor sample.            */
 typedef struct {
-  uint64_t seed, round;
-  int lo, count, stride, B;
-  int32_t *d_rows;
-} sh_next_rows;
+  int16_t *d_undo;
+  int32_t *next_rows;
+  uint64_t next_seed, next_round;
+  int next_lo, next_count, next_stride, next_B;
+  int publish, publish_slot;
+  int64_t publish_seq;
+} sh_round_ext;
 int sh_solve_round(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, int16_t *d_types,
-                   int32_t *d_col, int64_t *d_cost, int64_t *d_delta, int64_t *d_steps, int16_t *d_undo,
-                   const sh_next_rows *next, unsigned flags, void *stream);
+                   int32_t *d_col, int64_t *d_cost, int64_t *d_delta, int64_t *d_steps,
+                   const sh_round_ext *ext, unsigned flags, void *stream);
 
 /* The kernel design sh_solve_blocks uses for these arguments (SH_DESIGN_*),
  * or < 0 on bad arguments.  Singles n <= 256 default to the sparse kernel

@@ -1179,6 +1179,12 @@ struct SantaArgs {
   int32_t *nx_rows;       // [nx_total] or null
   ShFeistel nx_f;
   int nx_lo, nx_stride, nx_total;
+  // sh_solve_round's publish, folded into the fallback launch (santa_vt_kernel
+  // <0, 0>): its last workgroup to finish writes the round's delta sums into
+  // the host mailbox (see publish_delta).  pub_mail null: no publish.
+  int64_t *pub_mail;
+  int64_t pub_seq;
+  int32_t *pub_cnt;       // workgroups finished (the context's err[2]; reset by the last)
 };
 
 // The round's prologue of every Santa block kernel (sh_solve_round), before
@@ -2012,6 +2018,20 @@ __device__ __forceinline__ void santa_vt_block(const SantaArgs &a, const int b) 
   }
 }
 
+// The round's delta sums d[0..1] into a host mailbox slot (coherent mapped
+// host memory): values first, the sequence number last with a system-scope
+// release, so the polling host sees seq only together with the values; then
+// the delta is zeroed for its next round.  One lane; vector stores.
+__device__ inline void publish_delta(int64_t *d, int64_t *mail, int64_t seq) {
+  const int64_t v0 = __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t v1 = __hip_atomic_load(d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(mail + 1, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(mail + 2, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(mail, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(d, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(d + 1, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // SV = 1 (the 4-wave register-tile design's launch): one workgroup per block.
 // SV = 0 is only ever the fallback launch (a.blist: the blocks another launch
 // left, count *a.bcount, usually 0): a small grid that loops over the list,
@@ -2029,6 +2049,15 @@ __global__ __launch_bounds__(VT_WG, SV == 0 ? 1 : 4) void santa_vt_kernel(SantaA
     for (int q = blockIdx.x; q < cnt; q += gridDim.x) {
       santa_vt_block<MODE, SV>(a, a.blist[q]);
       __syncthreads();  // (LDS reused by the next listed block)
+    }
+    if (a.pub_mail && threadIdx.x == 0) {
+      // this workgroup's delta atomics are ordered before its count (release);
+      // the last workgroup (acquire) then sees every workgroup's
+      const int done = __hip_atomic_fetch_add(a.pub_cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (done == (int)gridDim.x - 1) {
+        publish_delta(a.delta, a.pub_mail, a.pub_seq);
+        __hip_atomic_store(a.pub_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   } else {
     round_prologue(a, blockIdx.x, MODE);
@@ -5044,14 +5073,7 @@ __global__ void sample_kernel(ShFeistel f, int lo, int stride, int total, int32_
 // release: the host sees it only with the values), then the delta zeroed for
 // its next round.  One lane; vector stores.
 __global__ void publish_kernel(int64_t *d, int64_t *mail, int64_t seq) {
-  if (threadIdx.x == 0) {
-    const int64_t v0 = d[0], v1 = d[1];
-    __hip_atomic_store(mail + 1, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(mail + 2, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(mail, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    d[0] = 0;
-    d[1] = 0;
-  }
+  if (threadIdx.x == 0) publish_delta(d, mail, seq);
 }
 
 __global__ void pack_kernel(const int16_t *types, const int32_t *rows, int count, int16_t *out) {
@@ -5538,8 +5560,6 @@ int launch_santa_lb(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
     f.ovf_reset = ctx->d_ovf + (p ^ 1);
     f.undo = nullptr;
     f.nx_rows = nullptr;
-  f.undo = nullptr;
-  f.nx_rows = nullptr;
     rc = launch_big_list(ctx, f, B, s);
   }
   if (rc) {
@@ -5857,25 +5877,31 @@ extern "C" {
 int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, int16_t *d_types,
                     int32_t *d_col, int64_t *d_cost, int64_t *d_delta, int64_t *d_steps,
                     unsigned flags, void *stream) {
-  return sh_solve_round(ctx, mode, d_rows, n, B, d_types, d_col, d_cost, d_delta, d_steps, nullptr, nullptr,
-                        flags, stream);
+  return sh_solve_round(ctx, mode, d_rows, n, B, d_types, d_col, d_cost, d_delta, d_steps, nullptr, flags, stream);
 }
 
 int sh_solve_round(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, int16_t *d_types,
-                   int32_t *d_col, int64_t *d_cost, int64_t *d_delta, int64_t *d_steps, int16_t *d_undo,
-                   const sh_next_rows *next, unsigned flags, void *stream) {
+                   int32_t *d_col, int64_t *d_cost, int64_t *d_delta, int64_t *d_steps, const sh_round_ext *ext,
+                   unsigned flags, void *stream) {
   if (!ctx || (!d_rows && B > 0) || !d_types) return fail(SH_ERR_ARGS, "null pointer");
-  if (next && (!next->d_rows || next->B < 0 || next->count <= 0 || next->stride <= 0 ||
-               (int64_t)n * next->B > next->count))
+  const bool sample = ext && ext->next_rows && ext->next_B > 0;
+  if (sample && (ext->next_count <= 0 || ext->next_stride <= 0 || (int64_t)n * ext->next_B > ext->next_count))
     return fail(SH_ERR_ARGS, "bad next-round sampler arguments");
+  const bool publish = ext && ext->publish;
+  if (publish && (!d_delta || ext->publish_slot < 0 || ext->publish_slot > 1))
+    return fail(SH_ERR_ARGS, "bad mailbox arguments");
   if (mode != SH_MODE_SINGLE && mode != SH_MODE_TWINS && mode != SH_MODE_TRIPLETS)
     return fail(SH_ERR_ARGS, "bad mode");
   if (n <= 0 || n > SH_MAX_N_SANTA) return fail(SH_ERR_ARGS, "n must be in [1, 4096]");
   if ((int64_t)n * (mode + 1) > ctx->nc) return fail(SH_ERR_ARGS, "block larger than the instance");
   if (B < 0) return fail(SH_ERR_ARGS, "B < 0");
   HIP_TRY_RC(refuse_retired(flags));
-  if (B == 0) return SH_OK;
   DeviceGuard dg(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (B == 0) {
+    if (publish) HIP_TRY_RC(sh_publish_delta(ctx, d_delta, ext->publish_slot, ext->publish_seq, stream));
+    return SH_OK;
+  }
   SantaArgs a;
   a.rows = d_rows; a.types = d_types; a.col = d_col; a.cost = d_cost; a.delta = d_delta;
   a.steps = d_steps; a.wish = ctx->d_wish; a.wish10 = ctx->d_wish10; a.csr_off = ctx->d_csr_off; a.csr = ctx->d_csr;
@@ -5883,32 +5909,49 @@ int sh_solve_round(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, i
   a.n_wish = ctx->n_wish; a.n_good = ctx->n_good; a.flags = flags;
   a.cap = 0; a.ovf_cnt = nullptr; a.ovf_list = nullptr;
   a.blist = nullptr; a.bcount = nullptr; a.ovf_reset = nullptr;
-  a.undo = d_undo;
+  a.undo = ext ? ext->d_undo : nullptr;
   a.nx_rows = nullptr;
   a.nx_lo = a.nx_stride = a.nx_total = 0;
   a.nx_f = ShFeistel{};
-  if (next && next->B > 0) {
-    a.nx_rows = next->d_rows;
-    a.nx_f = sh_feistel_make(next->seed, next->round, (uint64_t)next->count);
-    a.nx_lo = next->lo;
-    a.nx_stride = next->stride;
-    a.nx_total = n * next->B;
+  if (sample) {
+    a.nx_rows = ext->next_rows;
+    a.nx_f = sh_feistel_make(ext->next_seed, ext->next_round, (uint64_t)ext->next_count);
+    a.nx_lo = ext->next_lo;
+    a.nx_stride = ext->next_stride;
+    a.nx_total = n * ext->next_B;
   }
-  hipStream_t s = (hipStream_t)stream;
-  switch (pick_design(ctx, mode, n, B, flags)) {
+  a.pub_mail = nullptr;
+  a.pub_seq = 0;
+  a.pub_cnt = ctx->d_err + 2;
+  const int design = pick_design(ctx, mode, n, B, flags);
+  // designs whose last launch is the fallback santa_vt_kernel<0, 0>: its last
+  // workgroup publishes (one launch fewer between two rounds); the others
+  // enqueue publish_kernel after their launches
+  const bool fold = design == SH_DESIGN_SPARSE || design == SH_DESIGN_SPARSE3 || design == SH_DESIGN_DT_TILE ||
+                    design == SH_DESIGN_VT_TILE;
+  if (publish && fold) {
+    a.pub_mail = ctx->d_mail + 4 * ext->publish_slot;
+    a.pub_seq = ext->publish_seq;
+  }
+  int rc;
+  switch (design) {
     case SH_DESIGN_LARGE:
-      return mode == SH_MODE_SINGLE ? launch_santa_big<0>(ctx, a, B, s)
-             : mode == SH_MODE_TWINS ? launch_santa_big<1>(ctx, a, B, s)
-                                     : launch_santa_big<2>(ctx, a, B, s);
-    case SH_DESIGN_LARGE_LB: return launch_santa_lb(ctx, a, B, s);
-    case SH_DESIGN_TWINS: return launch_santa<1, 1>(ctx, a, B, s);
+      rc = mode == SH_MODE_SINGLE ? launch_santa_big<0>(ctx, a, B, s)
+           : mode == SH_MODE_TWINS ? launch_santa_big<1>(ctx, a, B, s)
+                                   : launch_santa_big<2>(ctx, a, B, s);
+      break;
+    case SH_DESIGN_LARGE_LB: rc = launch_santa_lb(ctx, a, B, s); break;
+    case SH_DESIGN_TWINS: rc = launch_santa<1, 1>(ctx, a, B, s); break;
     case SH_DESIGN_LDS_TILE:
-      return (flags & SH_FLAG_TIMING) ? launch_santa<1, 0, true>(ctx, a, B, s) : launch_santa<1, 0>(ctx, a, B, s);
-    case SH_DESIGN_VT_TILE: return launch_santa_vt_sc(ctx, a, B, s);
-    case SH_DESIGN_DT_TILE: return launch_santa_dt(ctx, a, B, s);
-    case SH_DESIGN_SPARSE3: return launch_santa_sp(ctx, a, B, s, true);
-    default: return launch_santa_sp(ctx, a, B, s, false);
+      rc = (flags & SH_FLAG_TIMING) ? launch_santa<1, 0, true>(ctx, a, B, s) : launch_santa<1, 0>(ctx, a, B, s);
+      break;
+    case SH_DESIGN_VT_TILE: rc = launch_santa_vt_sc(ctx, a, B, s); break;
+    case SH_DESIGN_DT_TILE: rc = launch_santa_dt(ctx, a, B, s); break;
+    case SH_DESIGN_SPARSE3: rc = launch_santa_sp(ctx, a, B, s, true); break;
+    default: rc = launch_santa_sp(ctx, a, B, s, false); break;
   }
+  if (rc == SH_OK && publish && !fold) rc = sh_publish_delta(ctx, d_delta, ext->publish_slot, ext->publish_seq, stream);
+  return rc;
 }
 
 int sh_solve_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {

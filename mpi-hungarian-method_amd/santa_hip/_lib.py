@@ -87,7 +87,7 @@ SIGNATURES = {
     "sh_sample_blocks": (_I, [_U64, _U64, _I, _I, _I, _I, _I, _P, _P]),
     "sh_sample_blocks_undo": (_I, [_U64, _U64, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
     "sh_solve_blocks": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _U, _P]),
-    "sh_solve_round": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _U, _P]),
+    "sh_solve_round": (_I, [_P, _I, _P, _I, _I, _P, _P, _P, _P, _P, _P, _U, _P]),
     "sh_score": (_I, [_P, _P, _P, _P]),
     "sh_ctx_error_flags": (_I, [_P, _P]),
     "sh_ctx_mailbox": (ctypes.POINTER(ctypes.c_int64), [_P]),
@@ -106,11 +106,14 @@ SIGNATURES = {
 }
 
 
-class NextRows(ctypes.Structure):
-    """sh_next_rows (include/santa_hip.h): the next round's sampler arguments."""
-    _fields_ = [("seed", ctypes.c_uint64), ("round", ctypes.c_uint64), ("lo", ctypes.c_int),
-                ("count", ctypes.c_int), ("stride", ctypes.c_int), ("B", ctypes.c_int),
-                ("d_rows", ctypes.c_void_p)]
+class RoundExt(ctypes.Structure):
+    """sh_round_ext (include/santa_hip.h): sh_solve_round's undo record,
+    next-round sampler arguments and mailbox publish."""
+    _fields_ = [("d_undo", ctypes.c_void_p), ("next_rows", ctypes.c_void_p),
+                ("next_seed", ctypes.c_uint64), ("next_round", ctypes.c_uint64),
+                ("next_lo", ctypes.c_int), ("next_count", ctypes.c_int), ("next_stride", ctypes.c_int),
+                ("next_B", ctypes.c_int), ("publish", ctypes.c_int), ("publish_slot", ctypes.c_int),
+                ("publish_seq", ctypes.c_int64)]
 
 
 class SantaHipError(RuntimeError):

@@ -155,11 +155,12 @@ class SantaGPU:
                     undo: torch.Tensor | None = None, next_round: tuple | None = None,
                     col: torch.Tensor | None = None, cost: torch.Tensor | None = None,
                     delta: torch.Tensor | None = None, steps: torch.Tensor | None = None,
-                    flags: int = 0) -> None:
-        """solve_blocks + the loop's round bookkeeping in the same launch
-        (sh_solve_round): undo[k] = the round's starting type at rows[k], and
+                    publish: tuple | None = None, flags: int = 0) -> None:
+        """solve_blocks + the loop's round bookkeeping in the same launches
+        (sh_solve_round): undo[k] = the round's starting type at rows[k];
         next_round = (seed, round, B, out) samples that round's rows into out
-        (the values sample_blocks writes)."""
+        (the values sample_blocks writes); publish = (slot, seq) publishes
+        delta into the mailbox afterwards (publish_delta's effect)."""
         assert rows.dtype == torch.int32 and rows.is_contiguous() and rows.device == self.device
         assert types.dtype == torch.int16 and types.numel() == self.nc and types.device == self.device
         B = rows.numel() // n
@@ -168,17 +169,23 @@ class SantaGPU:
                             (steps, torch.int64, B), (undo, torch.int16, B * n)):
             if t is not None:
                 assert t.dtype == dt and t.numel() >= size and t.device == self.device
-        nx = None
+        ext = _lib.RoundExt()
+        ext.d_undo = undo.data_ptr() if undo is not None else None
         if next_round is not None:
             seed, rnd, Bn, out = next_round
             lo, count, stride, nb = self.geometry(mode, n)
             if Bn > nb:
                 raise ValueError(f"only {nb} disjoint blocks of {n} exist, asked for {Bn}")
             assert out.dtype == torch.int32 and out.numel() >= Bn * n and out.device == self.device
-            nx = _lib.NextRows(seed, rnd, lo, count, stride, Bn, out.data_ptr())
+            ext.next_rows = out.data_ptr()
+            ext.next_seed, ext.next_round = seed, rnd
+            ext.next_lo, ext.next_count, ext.next_stride, ext.next_B = lo, count, stride, Bn
+        if publish is not None:
+            assert delta is not None
+            ext.publish = 1
+            ext.publish_slot, ext.publish_seq = int(publish[0]), int(publish[1])
         rc = _lib.lib().sh_solve_round(self._h, mode, _ptr(rows), n, B, _ptr(types), _ptr(col), _ptr(cost),
-                                       _ptr(delta), _ptr(steps), _ptr(undo),
-                                       ctypes.byref(nx) if nx is not None else None,
+                                       _ptr(delta), _ptr(steps), ctypes.byref(ext),
                                        _lib.SH_COMPAT_TIEBREAK | flags, self.stream)
         _lib.check(rc, "sh_solve_round")
 

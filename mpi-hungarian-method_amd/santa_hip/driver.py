@@ -303,6 +303,7 @@ def run_rounds(engine, types: torch.Tensor, *, mode: int = _lib.SH_MODE_SINGLE, 
         if backup is not None and tok is None:
             backup.copy_(types)
         d = sums.buffer(0) if sums.delta else None
+        _announce(engine, d, sums, world, rnd, snapshot=False)
         if b1 > b0:
             engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types, delta=d)
         if world.distributed:
@@ -361,6 +362,16 @@ def _sample(engine, mode, n, B, seed, rnd, types):
     return sr(mode, n, B, seed, rnd, types)
 
 
+def _announce(engine, d, sums, world, rnd, snapshot) -> None:
+    """Before a round's solve, tell an engine with a host mailbox
+    (GPUEngine.announce_delta) how the round's delta d will be read -- the
+    arguments its delta_begin will get -- so that the mailbox publish can
+    ride on the round's last launch."""
+    a = getattr(engine, "announce_delta", None)
+    if a is not None and d is not None:
+        a(d, sums.check_round(rnd), world.distributed, snapshot)
+
+
 def _drain(engine) -> None:
     """Engines with side-stream work (GPUEngine.drain) finish it before the
     loop returns and its delta buffers are released."""
@@ -397,6 +408,7 @@ def _run_pipelined(engine, types, mode, n, B, seed, max_rounds, patience, world,
         if check_disjoint:
             assert_disjoint(rows, mode)
         d = sums.buffer(k) if sums.delta else None
+        _announce(engine, d, sums, world, r, snapshot=not undo_mode)
         if b1 > b0:
             engine.solve_blocks(mode, rows[b0 * n:b1 * n], n, types, delta=d)
         if world.distributed:
@@ -647,6 +659,8 @@ class GPUEngine:
         them, and sample the next round's rows (sh_solve_round)."""
         cur = self._cur
         self._cur = None
+        ann = self._announced
+        self._announced = None
         full = (cur is not None and self.FUSED_SAMPLING and rows.numel() == cur[4] * n
                 and rows.data_ptr() == self._pf_buf[cur[0]].data_ptr())
         if not full:
@@ -663,8 +677,12 @@ class GPUEngine:
                 nxt = (seed, rnd + 1, B, self._pf_buf[k1])
                 self._pf_rnd[k1] = rnd + 1
                 self._by_solve[k1] = True
+        pub = None
+        if ann is not None and delta is not None and ann == (delta.data_ptr(), True):
+            pub = self._next_mail()
+            self._prepub = (delta.data_ptr(),) + pub
         self.ctx.solve_round(mode, rows, n, types, undo=self._undo_buf[k] if undo_pending else None,
-                             next_round=nxt, delta=delta, steps=steps)
+                             next_round=nxt, delta=delta, steps=steps, publish=pub)
 
     def new_delta(self):
         return torch.zeros(2, dtype=torch.int64, device=self.ctx.device)
@@ -710,16 +728,34 @@ class GPUEngine:
     # round's kernels, polled by the host) instead of an event, a second
     # stream's copy and a cross-stream wait between two rounds' kernels
     MAILBOX = True
+    _announced = None  # (delta address, read through the mailbox) of the next solve
+    _prepub = None  # (delta address, slot, seq) published by the last solve_round
 
-    def _publish(self, d):
+    def announce_delta(self, d, full: bool, reduced: bool, snapshot: bool):
+        """The loop's delta_begin arguments for the round about to be solved
+        (run_rounds' _announce): a mailbox round solved whole by one
+        solve_round call publishes from that call's last launch (the fallback
+        launch's last workgroup), one launch fewer between two rounds."""
+        self._announced = (d.data_ptr(), bool(self.MAILBOX and not (full or reduced or snapshot)))
+
+    def _next_mail(self):
         ctx = self.ctx
         slot = getattr(self, "_mslot", 0)
         self._mslot = slot ^ 1
         seq = getattr(ctx, "_mail_seq", 0) + 1  # (per context: unique across engines)
         ctx._mail_seq = seq
-        ctx.publish_delta(d, slot, seq)
-        self._zero_ev[d.data_ptr()] = _ZEROED  # (zeroed by the publish kernel, in stream order)
-        mail = ctx.mailbox
+        return slot, seq
+
+    def _publish(self, d):
+        pre = self._prepub
+        self._prepub = None
+        if pre is not None and pre[0] == d.data_ptr():
+            slot, seq = pre[1:]
+        else:
+            slot, seq = self._next_mail()
+            self.ctx.publish_delta(d, slot, seq)
+        self._zero_ev[d.data_ptr()] = _ZEROED  # (zeroed by the publish, in stream order)
+        mail = self.ctx.mailbox
 
         class _Handle:
             def result(_):
@@ -737,6 +773,9 @@ class GPUEngine:
     def _begin(self, types, d, full: bool, after=None, snapshot: bool = True):
         if self.MAILBOX and d is not None and after is None and not (full or snapshot):
             return self._publish(d)
+        if self._prepub is not None and d is not None and self._prepub[0] == d.data_ptr():
+            raise RuntimeError("delta_begin: the round's delta was already published to the mailbox "
+                               "(announce_delta announced a mailbox round)")
         if not hasattr(self, "_snaps"):
             dev = types.device
             self._side_stream()

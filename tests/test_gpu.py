@@ -1122,10 +1122,14 @@ def test_dense_tile_build_declines_to_the_chains(sh, ctx, full_data, mode, fl):
 def test_solve_round_bookkeeping(sh, ctx, full_data, mode, n, B, fl):
     """sh_solve_round (every design, its fallback launch too: SH_FLAG_TEST_RANGE):
     the same solve as sh_solve_blocks, the round's undo record equals the
-    starting types at its rows (and scattering it back undoes the round), and
-    the next round's rows equal sh_sample_blocks' for that round."""
+    starting types at its rows (and scattering it back undoes the round), the
+    next round's rows equal sh_sample_blocks' for that round, and the publish
+    (folded into the fallback launch, or its own kernel) puts the delta sums
+    into the mailbox behind the sequence number and zeroes the delta."""
     _, _, _, nb = ctx.geometry(mode, n)
     rows = ctx.sample_blocks(mode, n, B, 77, 3)
+    seq = (1 << 40) + B * 16 + fl % 16 + 4096 * n  # (unique per case)
+    mail = ctx.mailbox
     outs = []
     for fused in (False, True):
         types = ctx.upload_types(full_data.types)
@@ -1136,7 +1140,11 @@ def test_solve_round_bookkeeping(sh, ctx, full_data, mode, n, B, fl):
             undo = torch.full((B * n,), -7, dtype=torch.int16, device="cuda")
             nxt = torch.full((nb * n,), -1, dtype=torch.int32, device="cuda")
             ctx.solve_round(mode, rows, n, types, undo=undo, next_round=(77, 4, nb, nxt), col=col, cost=cost,
-                            delta=delta, flags=fl)
+                            delta=delta, publish=(1, seq), flags=fl)
+            torch.cuda.synchronize()
+            assert mail[4] == seq
+            assert delta.cpu().tolist() == [0, 0]
+            delta = torch.tensor([mail[5], mail[6]], dtype=torch.int64)
         else:
             ctx.solve_blocks(mode, rows, n, types, col=col, cost=cost, delta=delta, flags=fl)
         assert ctx.error_flags() == 0
