@@ -2051,12 +2051,17 @@ __global__ __launch_bounds__(VT_WG, SV == 0 ? 1 : 4) void santa_vt_kernel(SantaA
       __syncthreads();  // (LDS reused by the next listed block)
     }
     if (a.pub_mail && threadIdx.x == 0) {
-      // this workgroup's delta atomics are ordered before its count (release);
-      // the last workgroup (acquire) then sees every workgroup's
-      const int done = __hip_atomic_fetch_add(a.pub_cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (done == (int)gridDim.x - 1) {
-        publish_delta(a.delta, a.pub_mail, a.pub_seq);
-        __hip_atomic_store(a.pub_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cnt == 0) {  // (the usual case: the delta is complete since the launch before)
+        if (blockIdx.x == 0) publish_delta(a.delta, a.pub_mail, a.pub_seq);
+      } else if ((int)blockIdx.x < cnt) {
+        // the workgroups that solved listed blocks: each one's delta atomics
+        // are ordered before its count (release); the last (acquire) sees all
+        const int parts = min(cnt, (int)gridDim.x);
+        const int done = __hip_atomic_fetch_add(a.pub_cnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == parts - 1) {
+          publish_delta(a.delta, a.pub_mail, a.pub_seq);
+          __hip_atomic_store(a.pub_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
   } else {
