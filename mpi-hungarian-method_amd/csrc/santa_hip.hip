@@ -36,6 +36,15 @@
 #ifndef LB_CFG_2048
 #define LB_CFG_2048 0  // 1024 < n <= 2048: 0 = 8 waves x 4 columns, 1 = 4 x 8, 2 = 16 x 2
 #endif
+// santa_big_kernel, each wave loading its candidate's wishlist rows before the
+// fold (the winner's row then comes from LDS): 3000-pair twins lost 22 %
+// (4,064 -> 4,978 cycles per lone step, profiles/r05o_big_staged_ab.jsonl):
+// the step is bound by its 64-bit relaxation's VALU issue (16 waves on 4
+// SIMDs), not by the row's L2 hit, and staging adds a wave DPP minimum, the
+// loads and a barrier
+#ifndef BIG_STAGED
+#define BIG_STAGED 0
+#endif
 namespace {
 
 constexpr int WAVE = 64;
@@ -454,6 +463,22 @@ __device__ __forceinline__ uint64_t block_min_u64_rot(uint64_t wmin, uint64_t *s
   }
 }
 
+// Loaders with STAGED = true (WishRowLoader) let sap_solve_mw take the next
+// row's global load off the step's critical path: before the fold, every
+// wave issues the loads of its own candidate's row (prefetch, into
+// registers); the fold's winner is always one of the wave candidates, so
+// after the barrier the winning wave scatters the row it already holds
+// (scatter) and the next step only reads (read).  The first step of a
+// Dijkstra and a step decided by the exact argmin load as before (load).
+template <class L, class = void>
+struct staged_loader : std::false_type {};
+template <class L>
+struct staged_loader<L, std::void_t<decltype(L::STAGED)>> : std::bool_constant<L::STAGED> {};
+template <class L, bool S>
+struct staged_regs { static constexpr int value = 1; };
+template <class L>
+struct staged_regs<L, true> { static constexpr int value = L::PF; };
+
 template <int NW, int K, typename Loader, int FB = 10, typename... LA>
 __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, int64_t &steps_out,
                              int &fallbacks, const bool exact, const LA &...la) {
@@ -480,9 +505,13 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
   };
   int64_t steps = 0;
   int par = 0;  // rotating step-argmin word (0..2)
+  constexpr bool STG = staged_loader<Loader>::value && NW > 1;
+  int pf[staged_regs<Loader, STG>::value];  // (STG) the wave candidate's row, loaded before the fold
+  bool staged = false;           // (STG) this step's row was scattered by the last step's winner
   if (NW > 1 && tid < 3) S.red[tid] = ~0ull;
   __syncthreads();
   for (int cur = 0; cur < n; ++cur) {
+    staged = false;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int j = w * (WAVE * K) + k * WAVE + lane;
@@ -499,7 +528,14 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
       ++steps;
       const int64_t ui = S.u[i];
       int64_t c[K];
-      ld.load(i, c, la...);
+      if constexpr (STG) {
+        if (staged)
+          ld.read_staged(c);
+        else
+          ld.load(i, c);
+      } else {
+        ld.load(i, c, la...);
+      }
       if (NW > 1 && tid == 0) S.red[par == 2 ? 0 : par + 1] = ~0ull;
       const int64_t kU = minVal - ui;
       const uint64_t kb = (uint64_t)BIAS - (uint64_t)minVal;
@@ -525,8 +561,19 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
         best = (act && key < best) ? key : best;
       }
       uint64_t g;
+      uint64_t wm = ~0ull;  // (STG) this wave's candidate
       if constexpr (NW == 1) {
         g = wave_min_u64_fast<true>(best);
+      } else if constexpr (STG) {
+        // the wave's minimum; an assigned candidate's row loads while the
+        // fold's atomic and barrier run
+        wm = wave_min_u64_fast<true>(best);
+        const uint32_t wl = (uint32_t)wm;
+        if (wm != ~0ull && ((wl >> (2 * FB)) & 1u)) ld.prefetch((int)(wl & FM), pf);
+        if (lane == 0 && wm != ~0ull)
+          __hip_atomic_fetch_min(S.red + par, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __syncthreads();
+        g = S.red[par];
       } else {
         // DPP min of the high words within each 16-lane row; the lanes holding
         // it (usually one per row) fold their full keys into the step word
@@ -541,7 +588,8 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
       par = (par == 2) ? 0 : par + 1;
       const uint64_t hi = g >> LOB;
-      if (exact || (uint32_t)(g >> 32) - LOW >= SAT - LOW) {
+      const bool exact_step = exact || (uint32_t)(g >> 32) - LOW >= SAT - LOW;
+      if (exact_step) {
         // exact two-pass argmin: min spc (signed), then min key-low among ties
         uint64_t m = ~0ull;
 #pragma unroll
@@ -582,6 +630,11 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
         break;
       }
       i = aux;
+      if constexpr (STG) {
+        // (an exact step's winner need not be any wave's candidate)
+        staged = !exact_step;
+        if (staged && g == wm) ld.scatter(i, pf);
+      }
     }
     // Dual update (scipy: u[cur] += minVal; u[i] += minVal - spc[col4row[i]]
     // for the other visited rows; v[j] -= minVal - spc[j] for visited cols)
@@ -4089,11 +4142,28 @@ struct WishRowLoader {
   int n, nw, nw1;
   int64_t E;
   const int64_t *lut;     // twins: twin_lut_index -> exact cost (LDS), as the 4-wave twins kernel
+  int16_t *stage;         // LDS [M * nw] (STAGED): the winning wave's prefetched row
   static constexpr int M = MODE + 1;                     // children per unit
   static constexpr int BPC = MODE == 0 ? 1 : 2 * MODE;  // rowbuf bytes per column
+  static constexpr bool STAGED = BIG_STAGED != 0;
+  static constexpr int PF = 2 * M;                       // prefetch registers: ranks lane, lane + 64 per child
   static_assert(NW * WAVE >= (MODE + 1) * 127, "one thread per wish of a unit (n_wish <= 127)");
+  // the code of wish rank r of member vr to every column of gift type g
+  __device__ __forceinline__ void put(int g, int vr, int r) const {
+    const uint32_t h = thead[g];
+    const int cnt = (int)(h >> 16), e = (int)(h & 0xFFFFu);
+    const uint8_t code = (uint8_t)(r + 1);
+    // the type's first three columns read before any write (csort is padded:
+    // reads past the type are unused), the rest in a loop
+    const int b = e - cnt;
+    const int x0 = csort[b], x1 = csort[b + 1], x2 = csort[b + 2];
+    if (cnt > 0) rowbuf[BPC * x0 + vr] = code;
+    if (cnt > 1) rowbuf[BPC * x1 + vr] = code;
+    if (cnt > 2) rowbuf[BPC * x2 + vr] = code;
+    for (int x = b + 3; x < e; ++x) rowbuf[BPC * csort[x] + vr] = code;
+  }
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x;
     // one thread per wish of the unit's children (M * nw <= 381 < NW * 64):
     // a 2-byte load of the row (100 lanes read the 200 contiguous bytes), one
     // type-table read, the scatter of the code to the type's columns -- one
@@ -4102,19 +4172,45 @@ struct WishRowLoader {
       const int vr = tid / nw;  // member of the unit
       const int r = tid - vr * nw;
       // (32-bit offset: nc * n_wish < 2^31 is checked at sh_ctx_create)
-      const int g = wish[(uint32_t)(rows[i] + vr) * (uint32_t)nw + (uint32_t)r];
-      const uint32_t h = thead[g];
-      const int cnt = (int)(h >> 16), e = (int)(h & 0xFFFFu);
-      const uint8_t code = (uint8_t)(r + 1);
-      // the type's first three columns read before any write (csort is padded:
-      // reads past the type are unused), the rest in a loop
-      const int b = e - cnt;
-      const int x0 = csort[b], x1 = csort[b + 1], x2 = csort[b + 2];
-      if (cnt > 0) rowbuf[BPC * x0 + vr] = code;
-      if (cnt > 1) rowbuf[BPC * x1 + vr] = code;
-      if (cnt > 2) rowbuf[BPC * x2 + vr] = code;
-      for (int x = b + 3; x < e; ++x) rowbuf[BPC * csort[x] + vr] = code;
+      put(wish[(uint32_t)(rows[i] + vr) * (uint32_t)nw + (uint32_t)r], vr, r);
     }
+    read(c);
+  }
+  // (STAGED) the wave's candidate unit i: lane l loads ranks l and l + 64 of
+  // every member (-1 past n_wish); nothing waits for them here
+  __device__ __forceinline__ void prefetch(int i, int (&pf)[PF]) const {
+    const int lane = threadIdx.x & 63;
+    const uint32_t base = (uint32_t)rows[i] * (uint32_t)nw;
+#pragma unroll
+    for (int vr = 0; vr < M; ++vr) {
+      const int16_t *src = wish + base + (uint32_t)(vr * nw);
+      pf[2 * vr] = lane < nw ? src[lane] : -1;
+      pf[2 * vr + 1] = lane + WAVE < nw ? src[lane + WAVE] : -1;
+    }
+  }
+  // (STAGED) the winning wave writes the row it prefetched into the staging
+  // list (one gift per wish, as the distributed load reads them)
+  __device__ __forceinline__ void scatter(int, const int (&pf)[PF]) const {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int vr = 0; vr < M; ++vr) {
+      if (lane < nw) stage[vr * nw + lane] = (int16_t)pf[2 * vr];
+      if (lane + WAVE < nw) stage[vr * nw + lane + WAVE] = (int16_t)pf[2 * vr + 1];
+    }
+  }
+  // (STAGED) the next step's row from the staging list: every wish's type
+  // scattered by its own thread, as load() does after its global read
+  __device__ __forceinline__ void read_staged(int64_t (&c)[K]) const {
+    const int tid = threadIdx.x;
+    __syncthreads();
+    if (tid < M * nw) {
+      const int vr = tid / nw;
+      put(stage[tid], vr, tid - vr * nw);
+    }
+    read(c);
+  }
+  __device__ __forceinline__ void read(int64_t (&c)[K]) const {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     __syncthreads();
     // (every thread reads and clears its K slots: rowbuf covers NW * 64 * K
     //  columns, so no per-column branch; columns >= n are inactive)
@@ -4138,7 +4234,7 @@ struct WishRowLoader {
 };
 
 struct BigLds {
-  size_t u, c4r, r4c, path, red, rows, ctype, csort, thead, rowbuf, part, scan, lut, total;
+  size_t u, c4r, r4c, path, red, rows, ctype, csort, thead, rowbuf, part, scan, stage, lut, total;
 };
 
 // (the row buffer covers the NW * 64 * K columns the solver's threads own:
@@ -4158,6 +4254,7 @@ __host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int n
   L.rowbuf = o; o += r16((size_t)(nw * 64 * k) * (mode == 0 ? 1 : 2 * mode));
   L.part = o;   o += r16((size_t)nw * 3 * 8);
   L.scan = o;   o += r16((size_t)nw * 4);
+  L.stage = o;  o += r16((size_t)(mode + 1) * 128 * 2);
   L.lut = o;    o += mode == 1 ? (size_t)TWIN_LUT * 8 : 0;
   L.total = o;
   return L;
@@ -4321,7 +4418,8 @@ __device__ __forceinline__ void santa_big_block(const SantaArgs &a, const int b)
     for (int i = tid; i < n; i += WG) S.c4r[i] = (int16_t)i;
     __syncthreads();
   } else {
-    const WishRowLoader<MODE, NW, K> ld{a.wish, rows_l, thead, csort, rowbuf, n, a.n_wish, nw1, a.E, lut};
+    const WishRowLoader<MODE, NW, K> ld{a.wish, rows_l, thead, csort, rowbuf, n, a.n_wish, nw1, a.E, lut,
+                                        (int16_t *)(smem + L.stage)};
     sap_solve_mw<NW, K, WishRowLoader<MODE, NW, K>, FB>(n, ld, S, steps, fallbacks,
                                                          (a.flags & SH_FLAG_EXACT_ARGMIN) != 0);
   }
