@@ -460,27 +460,34 @@ def main():
             self.timed = False
             self.ev = []
 
-        # every EV_EVERY-th timed launch is bracketed by the events (and
-        # counts its steps): an event record is a marker packet on the stream,
-        # ~5 us of idle GPU between two rounds' kernels each (profiles/
-        # r05l_round_gaps.json against r05m's un-instrumented loop)
+        # every timed launch counts its Dijkstra steps; every EV_EVERY-th one
+        # from the EV_OFFSET-th on is also bracketed by the events: an event
+        # record is a marker packet on the stream, ~5 us of idle GPU between
+        # two rounds' kernels (profiles/r05l_round_gaps.json against r05m's
+        # un-instrumented loop).  Rounds 1, 5, 9, ...: round 0, twice as long
+        # as the rest, biased a sample that held it (the kernel average then
+        # came out above the round time)
         EV_EVERY = 4
+        EV_OFFSET = 1
 
         def solve_blocks(self, mode_, rows_, n_, types_, delta=None, steps=None):
-            self.calls = getattr(self, "calls", 0) + 1
-            if not self.timed or (self.calls - 1) % self.EV_EVERY:
+            if not self.timed:
                 return super().solve_blocks(mode_, rows_, n_, types_, delta=delta)
-            k = len(self.ev)
+            k = self.calls
+            self.calls += 1
+            st = steps_dev[k] if k < max_calls else None
+            if k % self.EV_EVERY != self.EV_OFFSET:
+                return super().solve_blocks(mode_, rows_, n_, types_, delta=delta, steps=st)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            super().solve_blocks(mode_, rows_, n_, types_, delta=delta,
-                                 steps=steps_dev[k] if k < max_calls else None)
+            super().solve_blocks(mode_, rows_, n_, types_, delta=delta, steps=st)
             e1.record(stream)
-            self.ev.append((e0, e1))
+            self.ev.append((e0, e1, k))
 
     eng = BenchEngine(ctx)
-    ev_every = BenchEngine.EV_EVERY
+    eng.calls = 0
+    eng.EV_OFFSET = BenchEngine.EV_OFFSET if args.steps > 1 else 0
     sc0, sg0, _, _ = ctx.score_sums(types)
     score0 = santa_hip.score_from_sums(sc0, sg0, ctx.nc, ctx.ng, ctx.n_wish, ctx.n_good)
 
@@ -523,7 +530,7 @@ def main():
     ev = eng.ev
     state = {"best": res.best_score}
     launches = len(ev)
-    kern_ms = [a.elapsed_time(b) for a, b in ev] or [0.0]
+    kern_ms = [a.elapsed_time(b) for a, b, _ in ev] or [0.0]
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
     blocks_total = nb * args.steps
     value = blocks_total / elapsed
@@ -541,8 +548,9 @@ def main():
     latency = None
     lds = None
     if my_blocks:
-        st = steps_dev[:min(launches, max_calls), :my_blocks].cpu().numpy().astype(np.int64)
-        bmax = int(st[0].argmax())
+        st_all = steps_dev[:min(eng.calls, max_calls), :my_blocks].cpu().numpy().astype(np.int64)
+        st = st_all[[k for _, _, k in ev if k < len(st_all)]]  # (the launches the events timed)
+        bmax = int(st_all[0].argmax())
         rows0 = ctx.sample_blocks(mode, n, nb, args.seed, 0)
         one = rows0[(b0 + bmax) * n:(b0 + bmax + 1) * n].contiguous()
         force = {0: _lib.SH_FLAG_SP_TILE, 7: _lib.SH_FLAG_SP_TILE, 1: _lib.SH_FLAG_LDS_TILE,
@@ -578,7 +586,7 @@ def main():
                 lds["pmc"] = occ
         latency = {"steps_per_launch": float(st.sum(axis=1).mean()),
                    "steps_max_block_per_launch": float(st.max(axis=1).mean()),
-                   "round0_steps": int(st[0].sum()), "round0_max_block_steps": int(st[0].max()),
+                   "round0_steps": int(st_all[0].sum()), "round0_max_block_steps": int(st_all[0].max()),
                    "lone_block_steps": lone_steps, "lone_block_ms": round(min(lone) * 1e3, 4),
                    "cycles_per_step_lone": round(s_per_step * CLOCK_HZ, 1),
                    "resident_blocks": resident,
@@ -625,8 +633,9 @@ def main():
                                  "per block / kernel time); the kernel is bound by its serial "
                                  "Dijkstra chains, see latency",
                      "kernel": kname, "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
-                     "kernel_avg_over": f"HIP events around every {ev_every}th timed launch "
-                                        f"({launches} of {args.steps} rounds)",
+                     "kernel_avg_over": f"HIP events around every {eng.EV_EVERY}th timed launch from the "
+                                        f"{eng.EV_OFFSET}th ({launches} of {eng.calls}); the floors and LDS "
+                                        "bytes over the same launches",
                      "algorithmic_bytes_per_block": per_block, "latency": latency, "lds": lds},
         "cpu": cpu,
     }

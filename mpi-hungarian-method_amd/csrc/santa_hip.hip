@@ -3101,10 +3101,12 @@ __device__ __forceinline__ uint32_t tile2_get(const u32x32 &T0, const u32x32 &T1
 // Per step: ~70 VALU (round 2's 64-bit santa_sp2_kernel: 108), no 64-bit LDS traffic.
 // ---------------------------------------------------------------------------
 // TIMED (SH_FLAG_TIMING, dev): shader-clock cycles per segment of the solve,
-// summed over the block, in col[b * n + 0..3]: A = a step's row fetch, scatter
-// and LDS reads up to the relaxation's inputs; B = relaxation, key and argmin;
-// C = winner decode and book-keeping; D = per-Dijkstra set-up, dual update and
-// augmentation.  (s_memtime stamps cost cycles themselves: relative view.)
+// summed over the block, in col[b * n + 0..6]: A = a step's row fetch, scatter
+// and LDS reads up to the relaxation's inputs (A1, col 4: the tile fetch and
+// the entry's fields); B = relaxation, key and argmin; C = winner decode and
+// book-keeping; per Dijkstra D0 (col 3) = set-up, D1 (col 5) = the dual
+// update, D2 (col 6) = the augmentation.  (s_memtime stamps cost cycles
+// themselves: relative view.)
 // Issue priority falls over the block's last Dijkstras (n-32, n-8, n-2): the
 // four blocks sharing a SIMD share its VALU issue, and a block near its end
 // has the least work left, so the blocks that lag behind (the long ones,
@@ -3435,7 +3437,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   const LatticeRange LR(Mm);  // |m(W)| + |m(u~)| + 1 <= M, as OR-accumulated bit tests
   __syncthreads();
   __builtin_amdgcn_s_setprio(3);  // (lowered over the last Dijkstras, below)
-  uint64_t tA = 0, tB = 0, tC = 0, tD = 0, tA1 = 0, ts = 0;
+  uint64_t tA = 0, tB = 0, tC = 0, tD = 0, tA1 = 0, tD1 = 0, tD2 = 0, ts = 0;
   auto stamp = [&](uint64_t &acc) {
     if constexpr (TIMED) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
@@ -3547,7 +3549,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         // The step's LDS traffic as one issue group for every row (a row with
         // more than 32 hits has the marker, whose slot is a dump slot, in its
         // entry 31; such a row re-reads its columns below): the dual and the
-        // mover, the scatter, the row reads, the un-scatter, the step's row
+        // mover, the scatter, the row reads (two ds_read_b64 of slots 2l, 2l+1
+        // and 128+2l, 129+2l: one bank per lane of a 32-lane group, where the
+        // ds_read2_b32 pairs were 2-way on both halves), the un-scatter, the step's row
         // (rowq[nrem - 1] = the dual's address) -- no wait in between; then
         // the previous step's book-keeping in their shadow, one lane and one
         // register each (exec = that lane, the slot by GPR indexing on the lo
@@ -3565,8 +3569,8 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
             "ds_read_b32 %0, %6\n\t"
             "ds_read_b32 %1, %7\n\t"
             "ds_write_b32 %8, %9\n\t"
-            "ds_read2_b32 %2, %10 offset1:1\n\t"
-            "ds_read2_b32 %3, %10 offset0:128 offset1:129\n\t"
+            "ds_read_b64 %2, %10\n\t"
+            "ds_read_b64 %3, %10 offset:512\n\t"
             "ds_write_b32 %8, %11\n\t"
             "ds_write_b32 %7, %6 offset:1024\n\t"
             "s_mov_b64 %4, exec\n\t"
@@ -3652,6 +3656,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         i = __builtin_amdgcn_readlane((int)rsel, lw);
         if (!assigned) break;
       }
+      stamp(tC);
       // Dual update (scipy's, in V units, deferred to the Dijkstra's end): the
       // columns that left `remaining` (lo = ~0; not the sink, whose update is
       // 0) add minVal - spc to -v and to the dual of their row.  Then each
@@ -3700,12 +3705,13 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
             : "+v"(LI), "=&s"(sv)
             : "s"(1ull << (sink >> 2)), "s"(sink & 3), "v"(LI.x));
       }
+      stamp(tD1);
       // augment along the path from the sink back to cur (registers only; at
       // most n hops -- a path that does not reach cur in n hops can only come
       // from values outside the checked range, and the block is left to the
       // fallback launch)
-      int j = sink, pi = -1;
-      for (int hop = 0; hop <= n; ++hop) {
+      int j = sink, pi = -1, left = n;
+      do {
         const int jl = j >> 2;
         int pv;  // prow[j & 3] (one indexed move), then lane jl of it
         asm volatile(
@@ -3728,9 +3734,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const uint32_t nr4 = (rw & ~(0xFFu << js)) | ((uint32_t)pi << js);
         asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(r4c) : "s"(nr4), "{m0}"(jl));
         j = t;
-        if (pi == cur) break;
-      }
+      } while (pi != cur && --left >= 0);
       bad |= pi != cur;
+      stamp(tD2);
     }
   }
   stamp(tD);
@@ -3799,9 +3805,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   if (lane == 0) {
     if (a.cost) a.cost[b] = cost;
     if (a.steps) a.steps[b] = steps;
-    if (TIMED && a.col && n >= 5) {
-      const uint64_t seg[5] = {tA, tB, tC, tD, tA1};
-      for (int q = 0; q < 5; ++q) a.col[(size_t)b * n + q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
+    if (TIMED && a.col && n >= 7) {
+      const uint64_t seg[7] = {tA, tB, tC, tD, tA1, tD1, tD2};
+      for (int q = 0; q < 7; ++q) a.col[(size_t)b * n + q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
     }
     if (a.delta) {
       atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);

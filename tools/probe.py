@@ -94,12 +94,13 @@ def main():
         t = base.clone()
         col = torch.zeros(B * a.n, dtype=torch.int32, device="cuda")
         ctx.solve_blocks(a.mode, rows, a.n, t, steps=steps, col=col, flags=_lib.SH_FLAG_TIMING | a.flags)
-        cv = col.view(B, a.n)[:, :5].cpu().numpy().astype(float)
+        cv = col.view(B, a.n)[:, :7].cpu().numpy().astype(float)
         sv = steps.cpu().numpy().astype(float)
         imax = int(sv.argmax())
         names = ["A_fetch_scatter_lds", "B_relax_argmin", "C_decode_bookkeeping", "D_per_dijkstra"]
         if (a.flags & 8) == 0:  # (santa_sp3_kernel: A split at the LDS issue, A1 = tile fetch + fields)
-            names = ["A2_lds_bookkeeping", "B_relax_argmin", "C_decode", "D_per_dijkstra", "A1_tile_fetch"]
+            names = ["A2_lds_bookkeeping", "B_relax_argmin", "C_decode", "D0_setup", "A1_tile_fetch",
+                     "D1_dual_update", "D2_augment"]
         cv = cv[:, :len(names)]
         out["segments_cycles_per_step"] = {nm: float(cv[:, q].sum() / sv.sum()) for q, nm in enumerate(names)}
         out["segments_cycles_per_step_maxblock"] = {nm: float(cv[imax, q] / sv[imax])
