@@ -45,6 +45,7 @@
 #ifndef BIG_STAGED
 #define BIG_STAGED 0
 #endif
+
 namespace {
 
 constexpr int WAVE = 64;
@@ -695,10 +696,24 @@ constexpr uint32_t SC_TIE_MASK = (1u << SC_SH) - 1u;
 constexpr uint64_t SC_BIAS = 1ull << (41 + SC_SH);
 constexpr int64_t SC_LIM = 1ll << (42 + SC_SH);
 
-template <int NW, typename Loader, typename... LA>
+// TIMED (dev): shader cycles of wave 0 per segment, summed over the solve, in
+// seg[0..4]: A = row dual and tile-row loads, the previous step's book-keeping,
+// up to the relaxation's inputs; B = relaxation, row argmin and the fold into
+// the step word; C = the barrier; D = the word's read, the ring re-arm and the
+// decode; E = per-Dijkstra set-up, dual update, augmentation and its barriers.
+template <int NW, bool TIMED = false, typename Loader, typename... LA>
 __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, const SolveLds &S, int64_t &steps_out,
-                                bool big, const LA &...la) {
+                                bool big, uint64_t *seg, const LA &...la) {
   const int tid = threadIdx.x, j = tid;
+  uint64_t tA = 0, tB = 0, tC = 0, tD = 0, tE = 0, ts = 0;
+  auto stamp = [&](uint64_t &acc) {
+    if constexpr (TIMED) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      acc += t - ts;
+      ts = t;
+    }
+  };
+  if constexpr (TIMED) ts = __builtin_amdgcn_s_memtime();
   const bool colv = j < n;
   int64_t sb = INT64_MAX, W = 0;  // spc + SC_BIAS; -v (this thread's column)
   int path = -1, pos = -1, r4c = -1;
@@ -725,7 +740,10 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
     // shadow of its row and dual loads (sap_solve_mw_l32's schedule)
     int pstar = -2, last = -3;
     uint32_t kX = 0;
+    bool first = true;
     for (;;) {
+      stamp(first ? tE : tD);
+      first = false;
       const int st = steps++;  // (this step's ring word: st % SC_RING)
       const uint64_t uraw = (uint64_t)S.u[i];
       int64_t c[1];
@@ -739,6 +757,10 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
                                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)uraw));
       uint64_t bse = SC_BIAS - (uint64_t)(ui - minVal);
       asm volatile("" : "+s"(bse));  // one SGPR pair: (W + c) + bse
+      if constexpr (TIMED) {
+        asm volatile("" ::"v"(c[0]), "s"(bse));
+        stamp(tA);
+      }
       const bool act = pos >= 0;
       // (a removed column never improves: r >= minVal >= its spc)
       const int64_t r = (int64_t)((uint64_t)(W + c[0]) + bse);
@@ -768,7 +790,9 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
             : "v"(bh), "v"(mh), "v"(wa), "v"(best)
             : "memory");
       }
+      stamp(tB);
       __syncthreads();
+      stamp(tC);
       uint64_t g;
       asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(g) : "v"(wa) : "memory");
       {
@@ -834,6 +858,14 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
       }
     }
     __syncthreads();
+  }
+  stamp(tE);
+  if constexpr (TIMED) {
+    seg[0] = tA;
+    seg[1] = tB;
+    seg[2] = tC;
+    seg[3] = tD;
+    seg[4] = tE;
   }
   big |= (uint64_t)(W + SC_LIM) >= 2 * (uint64_t)SC_LIM;
   if (colv) big |= (uint64_t)(S.u[j] + SC_LIM) >= 2 * (uint64_t)SC_LIM;
@@ -1590,7 +1622,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
   // -- solve ------------------------------------------------------------------
   int64_t steps = 0;
   int fallbacks = 0;
-  uint64_t seg[4] = {0, 0, 0, 0};  // (TIMED: sap_solve_mw_l32's segments)
+  uint64_t seg[5] = {0, 0, 0, 0, 0};  // (TIMED: sap_solve_mw_l32's / sap_solve_mw_sc's segments)
   const bool exact = (a.flags & SH_FLAG_EXACT_ARGMIN) != 0;
   if (a.flags & SH_FLAG_BUILD_ONLY) {  // phase timing: tile build + apply identity
     for (int i = tid; i < n; i += SANTA_WG) S.c4r[i] = (int16_t)i;
@@ -1608,7 +1640,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
         redo = sap_solve_mw_l32<SANTA_NW, TIMED>(n, ld, S, steps, force, a.E, seg);
       } else {
         const TileU16Loader<SANTA_NW, 1, SC_SH> ld{(const uint16_t *)tile8, E32, RS};
-        redo = sap_solve_mw_sc<SANTA_NW>(n, ld, S, steps, force);
+        redo = sap_solve_mw_sc<SANTA_NW, TIMED>(n, ld, S, steps, force, seg);
       }
     }
     if (redo) {
@@ -1683,8 +1715,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_block_kernel(SantaArgs a) {
       atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)td1);
     }
     if (fallbacks) atomicAdd(a.err + 1, fallbacks);
-    if (TIMED && a.col && n >= 4)  // (wave 0's segment cycles, see sap_solve_mw_l32)
-      for (int q = 0; q < 4; ++q) a.col[(size_t)b * n + q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
+    if (TIMED && a.col && n >= 5)  // (wave 0's segment cycles, see sap_solve_mw_l32 / _sc)
+      for (int q = 0; q < 5; ++q) a.col[(size_t)b * n + q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
   }
 }
 
@@ -6050,7 +6082,9 @@ int sh_solve_round(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, i
                                    : launch_santa_big<2>(ctx, a, B, s);
       break;
     case SH_DESIGN_LARGE_LB: rc = launch_santa_lb(ctx, a, B, s); break;
-    case SH_DESIGN_TWINS: rc = launch_santa<1, 1>(ctx, a, B, s); break;
+    case SH_DESIGN_TWINS:
+      rc = (flags & SH_FLAG_TIMING) ? launch_santa<1, 1, true>(ctx, a, B, s) : launch_santa<1, 1>(ctx, a, B, s);
+      break;
     case SH_DESIGN_LDS_TILE:
       rc = (flags & SH_FLAG_TIMING) ? launch_santa<1, 0, true>(ctx, a, B, s) : launch_santa<1, 0>(ctx, a, B, s);
       break;

@@ -98,7 +98,9 @@ def main():
         sv = steps.cpu().numpy().astype(float)
         imax = int(sv.argmax())
         names = ["A_fetch_scatter_lds", "B_relax_argmin", "C_decode_bookkeeping", "D_per_dijkstra"]
-        if (a.flags & 8) == 0:  # (santa_sp3_kernel: A split at the LDS issue, A1 = tile fetch + fields)
+        if a.mode == 1:  # (the 4-wave twins kernel, sap_solve_mw_sc: wave 0's segments)
+            names = ["A_dual_row_loads", "B_relax_rowmin_fold", "C_barrier", "D_word_decode", "E_per_dijkstra"]
+        elif (a.flags & 8) == 0:  # (santa_sp3_kernel: A split at the LDS issue, A1 = tile fetch + fields)
             names = ["A2_lds_bookkeeping", "B_relax_argmin", "C_decode", "D0_setup", "A1_tile_fetch",
                      "D1_dual_update", "D2_augment"]
         cv = cv[:, :len(names)]
