@@ -33,6 +33,14 @@
 #ifndef LB_PACKED
 #define LB_PACKED 0
 #endif
+// santa_lb_kernel, LB_DEFER: a wave's candidate row that is not staged is
+// loaded without a wait and written after the fold only if that wave won
+// (else at the next step's top), one more barrier on those steps: the
+// winner's row was such a load on 56 % of the steps (any wave's on 80 %,
+// tools/analysis/lb_stage_sim2.py), and it lost 4-7 % (profiles/r05s_lb_defer_ab.jsonl)
+#ifndef LB_DEFER
+#define LB_DEFER 0
+#endif
 #ifndef LB_CFG_2048
 #define LB_CFG_2048 0  // 1024 < n <= 2048: 0 = 8 waves x 4 columns, 1 = 4 x 8, 2 = 16 x 2
 #endif
@@ -4716,7 +4724,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
     uint32_t accU = 0, accW = 0;
     int par = 0;  // rotating step word
     uint64_t seg[6] = {0, 0, 0, 0, 0, 0}, ts = 0, ldlat = 0;
-    uint32_t nsync = 0, npre = 0;
+    uint32_t nsync = 0, npre = 0, nwin = 0;
     auto stamp = [&](int q) {
       if constexpr (TIMED) {
         const uint64_t x = __builtin_amdgcn_s_memtime();
@@ -4792,6 +4800,9 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         const uint32_t wmin = wave_min_u32_dpp(best);
         if constexpr (TIMED) asm volatile("" ::"s"(wmin));
         stamp(1);
+        // (LB_DEFER) this wave's candidate row, loaded this step without a
+        // wait: child pend (-1 none), gifts sg0/sg1, for table 2w + (slot & 1)
+        int pend = -1, sg0 = -1, sg1 = -1, pslot = 0;
         if (wmin != ~0u) {
           const int wl = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == wmin));
           int kk = K - 1;
@@ -4810,7 +4821,6 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
           const bool asg = (wmin >> 11) & 1u;
           int slot = 0;
           bool sync = false;
-          int sg0 = -1, sg1 = -1;
           uint64_t tl = 0;
           if (asg) {  // the candidate's row: staged in one of this wave's tables
             const int ch = (int)(inf >> 11);
@@ -4819,22 +4829,27 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
               v = 0;
             } else if (ch == chT1) {
               v = 1;
-            } else {  // not staged: load it now (on this step's chain)
+            } else {  // not staged: load it now
               v = lastSel ^ 1;  // the table not published last, unless the step reads it
               if (2 * w + v == tb) v ^= 1;
               if constexpr (TIMED) tl = __builtin_amdgcn_s_memtime();
               load_row(ch, sg0, sg1);
+#if LB_DEFER
+              pend = ch;  // (written after the fold if this wave wins, else at the next step's top)
+#else
               if (v == 0) chT0 = ch;
               else chT1 = ch;
               sync = true;
+#endif
               ++nsync;
             }
             lastSel = v;
             slot = 2 * w + v;
+            pslot = slot;
             if (lane == 0) tbl32[slot * (TS >> 1) + TU] = uu;
           }
           const uint64_t word = ((uint64_t)wmin << 32) | ((uint32_t)col << 17) | ((inf & 0x7FFu) << 6) |
-                                (uint32_t)slot;
+                                (pend >= 0 ? 32u : 0u) | (uint32_t)slot;
           if (lane == 0)
             __hip_atomic_fetch_min(words + par, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #if LB_PREFETCH
@@ -4893,7 +4908,25 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         const int gcol = (int)(gl >> 17);
         if (assigned) {  // the next step's row: its reads first
           i = (int)((gl >> 6) & 0x7FFu);
-          tb = (int)(gl & 63u);
+          tb = (int)(gl & 31u);
+#if LB_DEFER
+          // the winner's row was loaded this step without a wait (bit 5): its
+          // wave writes it into the table now, one more barrier for every wave
+          if ((gl >> 5) & 1u) {
+            if ((tb >> 1) == w) {
+              if ((tb & 1) == 0) {
+                write_row(tb, sg0, sg1, og0);
+                chT0 = pend;
+              } else {
+                write_row(tb, sg0, sg1, og1);
+                chT1 = pend;
+              }
+              pend = -1;
+              ++nwin;
+            }
+            __syncthreads();
+          }
+#endif
 #pragma unroll
           for (int k = 0; k < K; ++k) c[k] = tbl[tb * TS + ct[k]];
           ui = __builtin_amdgcn_readfirstlane(tbl32[tb * (TS >> 1) + TU]);
@@ -4920,6 +4953,14 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
             }
         }
         if (tid == 0 && pstar != last) rem[pstar] = (int16_t)mcol;
+#if LB_DEFER
+        if (pend >= 0) {  // a loaded row that did not win: into its table at the next step's top
+          pch = pend;
+          pZ = pslot & 1;
+          pg0 = sg0;
+          pg1 = sg1;
+        }
+#endif
         nrem = last;
         ++t;
         if (!assigned) {
@@ -4981,7 +5022,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         int32_t *o = a.col + (size_t)b * n + 8 * w;
         for (int q = 0; q < 6; ++q) o[q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
         o[6] = (int32_t)nsync;
-        o[7] = (int32_t)npre;
+        o[7] = (int32_t)(LB_DEFER ? nwin : npre);  // (LB_DEFER: steps this wave won with a row loaded that step)
         // (the synchronous loads' latency, issue to data, in col[b * n + 128 + w])
         a.col[(size_t)b * n + 128 + w] = (int32_t)min(ldlat, (uint64_t)INT32_MAX);
       }
