@@ -4802,7 +4802,8 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         stamp(1);
         // (LB_DEFER) this wave's candidate row, loaded this step without a
         // wait: child pend (-1 none), gifts sg0/sg1, for table 2w + (slot & 1)
-        int pend = -1, sg0 = -1, sg1 = -1, pslot = 0;
+        int pend = -1, sg0 = -1, sg1 = -1;
+        [[maybe_unused]] int pslot = 0;
         if (wmin != ~0u) {
           const int wl = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == wmin));
           int kk = K - 1;
