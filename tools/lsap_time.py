@@ -1,4 +1,5 @@
-"""dev: time lsap_solve_batched_hash for a few (n, B) on the library SANTA_HIP_LIB selects (A/B)."""
+"""dev: time lsap_solve_batched_hash for a few (n, B) on the library SANTA_HIP_LIB selects (A/B).
+    python tools/lsap_time.py [NxB ...]     (default: 256x512 512x256 1024x256 256x4096)"""
 import json
 import os
 import sys
@@ -8,7 +9,9 @@ sys.path.insert(0, os.path.join(ROOT, "mpi-hungarian-method_amd"))
 import torch  # noqa: E402
 import santa_hip  # noqa: E402
 
-for n, B in ((256, 512), (512, 256), (1024, 256), (256, 4096)):
+cases = [tuple(int(x) for x in c.split("x")) for c in sys.argv[1:]] or [(256, 512), (512, 256), (1024, 256),
+                                                                         (256, 4096)]
+for n, B in cases:
     santa_hip.solve_hash(7, 1 << 16, n, B)
     torch.cuda.synchronize()
     ts = []
