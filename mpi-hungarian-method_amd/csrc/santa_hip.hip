@@ -3523,6 +3523,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   // LDS group from the address it reads the dual with)
   uint32_t *rowq = rem + 256;
   const uint32_t ubase = lds_addr(u_l);
+  // (the two LDS bases a step's scalar indices are added to, in VGPRs: a
+  //  VOP3 takes one scalar operand)
+  uint32_t ubv = ubase, remv = lds_addr(rem);
+  asm volatile("" : "+v"(ubv), "+v"(remv));
   int steps = 0;
   // the lattice range left (per-lane flag); SH_FLAG_TEST_RANGE and
   // SH_FLAG_EXACT_ARGMIN send every block to the fallback launch (the
@@ -3600,7 +3604,8 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         // this rowq entry, rem[pstar] after the decode -- measured 5 % faster
         // per lone step than the same stores by one lane under an exec mask:
         // profiles/r04_ab_stores.jsonl.)
-        const uint32_t ua = ubase + 4u * (uint32_t)i;
+        uint32_t ua;  // (u_l + 4 i formed by one VALU: the address is a VGPR operand anyway)
+        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(ua) : "s"(i), "v"(ubv));
         const uint32_t ra = rq;
         const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
         const int32_t miss = SP3_MISS;
@@ -3687,7 +3692,11 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
         mmask = 1ull << (mv >> 2);
         kmv = mv & 3;
-        rem[pstar] = (uint32_t)mover_v;  // (every lane, same word; a no-op when pstar == last)
+        {  // rem[pstar] = mover (every lane, same word; a no-op when pstar == last)
+          uint32_t pa;
+          asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(pa) : "s"(pstar), "v"(remv));
+          asm volatile("ds_write_b32 %0, %1" ::"v"(pa), "v"(mover_v) : "memory");
+        }
         --nrem;
         rq -= 4u;
         // (branch-free: both the winner's column and its row are formed; the
