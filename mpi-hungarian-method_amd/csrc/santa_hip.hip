@@ -1826,7 +1826,7 @@ struct VtLds {
 // row i's cost of this thread's column from the register tile (x 2^SH);
 // singles only (the launcher never instantiates the twins register tile).
 // The tile's vectors come in as extra load() arguments (references passed
-// down the inlined call chain, as tile2_get takes them): a loader holding
+// down the inlined call chain): a loader holding
 // the tile, by reference or by value, put it in scratch.
 template <int SH>
 struct VtRegLoader {
@@ -3106,10 +3106,6 @@ __global__ __launch_bounds__(TILE_NW * WAVE) __attribute__((amdgpu_waves_per_eu(
 
 // T[q] for a wave-uniform q (one indexed VGPR move)
 // (both halves read with the same index and selected: no branch in the step)
-__device__ __forceinline__ uint32_t tile2_get(const u32x32 &T0, const u32x32 &T1, int q) {
-  const uint32_t a = T0[q & 31], b = T1[q & 31];
-  return (q & 32) ? b : a;
-}
 
 // ---------------------------------------------------------------------------
 // santa_sp3_kernel: one wave per block, the block's hit tile in 64 VGPRs
@@ -3532,13 +3528,14 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   // SH_FLAG_EXACT_ARGMIN send every block to the fallback launch (the
   // windowed-key solver, whose two-pass argmin the latter selects)
   bool bad = (a.flags & (SH_FLAG_TEST_RANGE | SH_FLAG_EXACT_ARGMIN)) != 0 || !LR.ok;
-  uint32_t accU = 0;  // OR of u~ + CU over every step (SGPR), see LatticeRange
+  uint32_t accU = 0;  // OR of u~ + CU over every step (a uniform VGPR), see LatticeRange
   uint32_t accW = 0;  // OR of W + CW over every Dijkstra (this lane's columns)
   // this lane's two row-buffer words (columns 4l, 4l+1 and 4l+2, 4l+3): kept
   // in registers across the loop (recomputed per step into a register still
   // read by the pending scatter, they made the compiler wait for it)
   int ro0 = 2 * lane;
   asm volatile("" : "+v"(ro0));
+  const uint32_t lhalf = (uint32_t)lane >> 5;  // (the 32-lane half: a row's entries live in one)
   const uint32_t rob = lds_addr(rowc) + 4u * (uint32_t)ro0;  // (LDS byte address)
   if (a.flags & SH_FLAG_BUILD_ONLY) {
     c4r = (uint32_t)(4 * lane) * 0x01010101u + 0x03020100u;
@@ -3556,7 +3553,8 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       *(uint4 *)(rem + 4 * ln) = rem0;
       int nrem = n;
       uint32_t rq = lds_addr(rem) + 4u * (uint32_t)(n - 1);  // &rem[nrem - 1], stepped down
-      int32_t minVal = 0;
+      asm volatile("" : "+v"(rq));  // (a VGPR: the LDS address operand, stepped by one VALU)
+      uint32_t mvb = (uint32_t)SP3_BIAS;  // minVal + BIAS (the key's value field of the last winner)
       int i = cur;
       int sink;
       // deferred book-keeping of the previous step, applied in the shadow of
@@ -3565,19 +3563,26 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       // winner's position (its pkey bits ^= kX); a lane mask of 0: none
       uint64_t wmask = 0, mmask = 0;
       int kw = 0, kmv = 0;
-      uint32_t kX = 0;
+      uint32_t kX = 0;  // (a VGPR: the xor's vector operand)
+      asm volatile("" : "+v"(kX));
       bool first = true;
       for (;;) {
         ++steps;
         stamp(first ? tD : tC);
         first = false;
-        const uint32_t tw = tile2_get(T0, T1, i >> 2);
+        // the tile dword of row i: T0 or T1 by bit 7 of i, one v_bfi with a
+        // sign-extended scalar mask (s_bfe_i32) instead of a compare and select
+        const uint32_t tw0 = T0[(i >> 2) & 31], tw1 = T1[(i >> 2) & 31];
+        const uint32_t tsel = (uint32_t)__builtin_amdgcn_sbfe(i, 7, 1);
+        uint32_t tw;  // (asm: the compiler turns the and/or form back into a compare and select)
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(tw) : "s"(tsel), "v"(tw1), "v"(tw0));
         // the entry's fields straight from the dword: a bit-field offset uses
         // bits 4:0 only, so i << 4 selects the 16-bit half (i & 1)
         const uint32_t sh = (uint32_t)i << 4;
         // the row's half of the wave (lanes 32L.., L = (i >> 1) & 1) as an SGPR mask
-        const uint32_t hl = (uint32_t)(-((i >> 1) & 1));
-        const bool mine = __builtin_amdgcn_inverse_ballot_w64(((uint64_t)hl << 32) | ~hl);
+        uint32_t hb;  // (bit 1 of i in a VGPR: the compare below is VALU, no scalar mask)
+        asm("v_bfe_u32 %0, %1, 1, 1" : "=v"(hb) : "s"(i));
+        const bool mine = lhalf == hb;
         const uint32_t ea = __builtin_amdgcn_ubfe(tw, sh + 9u, 7);
         // expand the row: hit columns get -a (key units), the rest hold a
         // miss; read this lane's four columns; put the misses back (in-order LDS)
@@ -3598,8 +3603,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         // ds_read2_b32 pairs were 2-way on both halves), the un-scatter, the step's row
         // (rowq[nrem - 1] = the dual's address) -- no wait in between; then
         // the previous step's book-keeping in their shadow, one lane and one
-        // register each (exec = that lane, the slot by GPR indexing on the lo
-        // tuple, %17 = its first register), one wait at the end.  Operands stay
+        // register each (a v_cndmask on that lane's mask, the slot by GPR
+        // indexing on the lo tuple, %17 = its first register; no exec
+        // changes: four SALU fewer), one wait at the end.  Operands stay
         // live through that wait.  (The one-word stores by all 64 lanes --
         // this rowq entry, rem[pstar] after the decode -- measured 5 % faster
         // per lone step than the same stores by one lane under an exec mask:
@@ -3609,7 +3615,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         const uint32_t ra = rq;
         const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
         const int32_t miss = SP3_MISS;
-        uint64_t sv;
+        uint32_t sv;  // (the mover's xor term: kX in its lane, 0 elsewhere)
         asm volatile(
             "ds_read_b32 %0, %6\n\t"
             "ds_read_b32 %1, %7\n\t"
@@ -3618,20 +3624,17 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
             "ds_read_b64 %3, %10 offset:512\n\t"
             "ds_write_b32 %8, %11\n\t"
             "ds_write_b32 %7, %6 offset:1024\n\t"
-            "s_mov_b64 %4, exec\n\t"
-            "s_mov_b64 exec, %12\n\t"
-            "s_set_gpr_idx_on %13, gpr_idx(DST)\n\t"
-            "v_mov_b32 %17, -1\n\t"
+            "v_cndmask_b32 %4, 0, %16, %14\n\t"
+            "s_set_gpr_idx_on %13, gpr_idx(SRC0,DST)\n\t"
+            "v_cndmask_b32 %17, %17, -1, %12\n\t"
             "s_set_gpr_idx_off\n\t"
-            "s_mov_b64 exec, %14\n\t"
             "s_set_gpr_idx_on %15, gpr_idx(SRC1,DST)\n\t"
-            "v_xor_b32 %17, %16, %17\n\t"
+            "v_xor_b32 %17, %4, %17\n\t"
             "s_set_gpr_idx_off\n\t"
-            "s_mov_b64 exec, %4\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "=&s"(sv), "+v"(lo)
+            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "=&v"(sv), "+v"(lo)
             : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(miss), "s"(wmask), "s"(kw), "s"(mmask),
-              "s"(kmv), "s"(kX), "v"(lo.x)
+              "s"(kmv), "v"(kX), "v"(lo.x)
             : "memory");
         // (a row with more than 32 hits: the tile's entries and the overflow
         // list scattered again, the four columns re-read; the other half's
@@ -3651,16 +3654,20 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           for (int x = lane; x < oc; x += WAVE) rowc[ovf[os + x] & 0x1FFu] = SP3_MISS;
         }
         const int32_t cc[4] = {c01.x, c01.y, c23.x, c23.y};
-        // u~[i] = u[i] - minVal (row i is reached at the current minimum)
-        const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
-        accU |= (uint32_t)ui + LR.CU;  // (the range of u~, scalar: two SALU)
+        // u~[i] = u[i] - minVal (row i is reached at the current minimum),
+        // its range and the step's value (BIAS - u~) in key units with the
+        // step t in the low byte: uniform values left in VGPRs -- four VALU
+        // instead of a readfirstlane and seven SALU (the scalar unit is the
+        // step's shared resource: every SALU removed shortened the round,
+        // profiles/r05t_sp3_valu_addr_ab.jsonl)
+        // (BIAS - u~ = mvb - u: the range term u~ + CU is (BIAS + CU) - that)
+        const uint32_t bu = mvb - (uint32_t)uraw;
+        accU |= ((uint32_t)SP3_BIAS + LR.CU) - bu;
+        const uint32_t bse = (bu << SP3_SH) | (uint32_t)(n - nrem);
         if constexpr (TIMED) {
-          asm volatile("" ::"v"(cc[0]), "v"(cc[3]), "s"(ui));
+          asm volatile("" ::"v"(cc[0]), "v"(cc[3]), "v"(bse));
           stamp(tA);
         }
-        // the step's scalar: (BIAS - u~) in key units, the step t in the low byte
-        uint32_t bse = ((uint32_t)(SP3_BIAS - ui) << SP3_SH) | (uint32_t)(n - nrem);
-        asm volatile("" : "+s"(bse));  // (Wp + c + bse: one add3 per column)
         uint32_t best = ~0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -3680,14 +3687,14 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           asm volatile("" ::"s"(g));
           stamp(tB);
         }
-        minVal = (int32_t)(g >> SP3_SH) - SP3_BIAS;
+        mvb = g >> SP3_SH;
         kw = (int)(g & 3u);
         const uint32_t pkey = (g >> 2) & 255u;
         const bool assigned = (g >> 10) & 1u;
         const int lw = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == g));
         const int pstar = assigned ? (int)pkey : 255 - (int)pkey;
         const int last = nrem - 1;
-        kX = (uint32_t)(last ^ pstar) << 2;
+        asm("v_lshlrev_b32 %0, 2, %1" : "=v"(kX) : "s"(last ^ pstar));
         wmask = 1ull << lw;
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
         mmask = 1ull << (mv >> 2);
@@ -3711,7 +3718,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       // 0) add minVal - spc to -v and to the dual of their row.  Then each
       // column's path row: the row of the step in sbp's low byte (rowq; an
       // unreached column reads an unused in-bounds word).
-      const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
+      const int32_t minVal = (int32_t)mvb - SP3_BIAS;
       i32x4 prow;  // (one VGPR tuple: the augmentation selects prow[j & 3] by an indexed move)
 #if SP3_MASKED_DUAL  // (the visited columns and the sink only; 1 % faster here,
                      //  2-4 % slower in santa_dt_kernel: profiles/r05h_masked_dual_ab.jsonl)

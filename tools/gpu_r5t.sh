@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-5 GPU session: santa_sp3_kernel step addresses formed in VALU (3 SALU
+# round-5 GPU session: santa_sp3_kernel SALU -> VALU (u~, bse, accU, rq, kX, tile half select):
 # fewer per step): parity, A/B against HEAD (abl/libsanta_hip_a.so), bench
 cd /root/repo
 export TMPDIR=/tmp
