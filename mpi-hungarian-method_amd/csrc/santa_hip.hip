@@ -4785,7 +4785,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         pch = __builtin_amdgcn_readfirstlane(pch);
         pZ = __builtin_amdgcn_readfirstlane(pZ);
         ++steps;
-        if (tid == 0) {
+        if (w == 0) {  // (every lane of wave 0, same words: a scalar branch, no exec mask)
           rowq[t] = (int16_t)i;
           words[par == 2 ? 0 : par + 1] = ~0ull;  // re-arm the next step's word
         }
@@ -4811,6 +4811,18 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
           key[k] = (sbp[k] & ~((1u << LB_TSH) - 1u)) | lo[k];
           best = min(best, key[k]);
         }
+        // per lane, the slot of its best key and that column's row info and
+        // u (VALU, in the DPP chain's shadow): the candidate is then three
+        // readlanes from the winning lane, no scalar compare-and-select chain
+        uint32_t kb = K - 1, ib = info[K - 1];
+        int32_t ub = ucol[K - 1];
+#pragma unroll
+        for (int k = K - 2; k >= 0; --k) {
+          const bool e = key[k] == best;
+          kb = e ? (uint32_t)k : kb;
+          ib = e ? info[k] : ib;
+          ub = e ? ucol[k] : ub;
+        }
         if constexpr (TIMED) asm volatile("" ::"v"(best));
         stamp(0);
         const uint32_t wmin = wave_min_u32_dpp(best);
@@ -4822,18 +4834,9 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         [[maybe_unused]] int pslot = 0;
         if (wmin != ~0u) {
           const int wl = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == wmin));
-          int kk = K - 1;
-#pragma unroll
-          for (int k = K - 2; k >= 0; --k)
-            if ((uint32_t)__builtin_amdgcn_readlane((int)key[k], wl) == wmin) kk = k;
-          uint32_t inf = 0;
-          int32_t uu = 0;
-#pragma unroll
-          for (int k = 0; k < K; ++k)
-            if (k == kk) {
-              inf = (uint32_t)__builtin_amdgcn_readlane((int)info[k], wl);
-              uu = __builtin_amdgcn_readlane(ucol[k], wl);
-            }
+          const int kk = __builtin_amdgcn_readlane((int)kb, wl);
+          const uint32_t inf = (uint32_t)__builtin_amdgcn_readlane((int)ib, wl);
+          const int32_t uu = __builtin_amdgcn_readlane(ub, wl);
           const int col = (w * K + kk) * WAVE + wl;
           const bool asg = (wmin >> 11) & 1u;
           int slot = 0;
@@ -4863,7 +4866,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
             lastSel = v;
             slot = 2 * w + v;
             pslot = slot;
-            if (lane == 0) tbl32[slot * (TS >> 1) + TU] = uu;
+            tbl32[slot * (TS >> 1) + TU] = uu;  // (every lane, same word)
           }
           const uint64_t word = ((uint64_t)wmin << 32) | ((uint32_t)col << 17) | ((inf & 0x7FFu) << 6) |
                                 (pend >= 0 ? 32u : 0u) | (uint32_t)slot;
@@ -4969,7 +4972,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
               asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(lo[k]) : "s"(x), "{m0}"(lm));
             }
         }
-        if (tid == 0 && pstar != last) rem[pstar] = (int16_t)mcol;
+        if (w == 0 && pstar != last) rem[pstar] = (int16_t)mcol;  // (wave 0, every lane)
 #if LB_DEFER
         if (pend >= 0) {  // a loaded row that did not win: into its table at the next step's top
           pch = pend;
