@@ -636,6 +636,7 @@ def main():
                      "kernel_avg_over": f"HIP events around every {eng.EV_EVERY}th timed launch from the "
                                         f"{eng.EV_OFFSET}th ({launches} of {eng.calls}); the floors and LDS "
                                         "bytes over the same launches",
+                     "kernel_avg_rounds": [k for _, _, k in ev],
                      "algorithmic_bytes_per_block": per_block, "latency": latency, "lds": lds},
         "cpu": cpu,
     }

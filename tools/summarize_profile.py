@@ -88,6 +88,11 @@ def main(src, tag, root):
             out["timed_window"] = {"kernels": kns, "launches": f"[{w}, {w + k})",
                                    "avg_ms": sum(t) / len(t),
                                    "bench_kernel_avg_ms": b["roofline"]["kernel_avg_ms"]}
+            rs = b["roofline"].get("kernel_avg_rounds")
+            if rs:  # the rounds the bench's events bracketed: the same launches in the trace
+                ts = [t[r] for r in rs if r < len(t)]
+                out["timed_window"]["event_rounds"] = rs
+                out["timed_window"]["event_rounds_avg_ms"] = sum(ts) / len(ts)
     fetch = pmc(os.path.join(src, "fetch_counter_collection.csv"))
     write = pmc(os.path.join(src, "write_counter_collection.csv"))
     fscore = pmc(os.path.join(src, "fetch_score_counter_collection.csv"))
