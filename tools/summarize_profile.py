@@ -43,7 +43,7 @@ def by_short(agg, main=None):
 
 def short(name):
     for key in ("santa_sp3_kernel", "santa_dt_kernel", "santa_sp2_kernel", "santa_tile_kernel", "santa_sp_kernel", "santa_vt_kernel", "santa_sw_kernel", "santa_block_kernel",
-                "santa_big_kernel", "score_kernel",
+                "santa_lb_kernel", "santa_big_kernel", "score_kernel", "publish_kernel",
                 "sample_kernel", "lsap_i64_kernel", "lsap_f64_kernel"):
         if key in name:
             return key
