@@ -761,12 +761,13 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
         lo ^= isM ? kX : 0u;  // (kX = 0 when the mover is the winner)
         pos = isW ? -1 : (isM ? pstar : pos);
       }
-      const int64_t ui = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uraw >> 32)) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)uraw));
-      uint64_t bse = SC_BIAS - (uint64_t)(ui - minVal);
-      asm volatile("" : "+s"(bse));  // one SGPR pair: (W + c) + bse
+      // (BIAS - u~) with u~ = u - minVal, left in VGPRs: the row dual is a
+      // uniform LDS value; VALU instead of two readfirstlanes and a 64-bit
+      // scalar subtraction (the four waves reach this point together after
+      // the barrier and share the CU's scalar unit)
+      const uint64_t bse = (SC_BIAS + (uint64_t)minVal) - uraw;
       if constexpr (TIMED) {
-        asm volatile("" ::"v"(c[0]), "s"(bse));
+        asm volatile("" ::"v"(c[0]), "v"(bse));
         stamp(tA);
       }
       const bool act = pos >= 0;
