@@ -839,7 +839,10 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
         sink = aux;
         break;
       }
-      i = aux;
+      // the next row from the word's VGPR copy: its dual and tile-row
+      // addresses are formed in VALU straight from the LDS read, not behind
+      // a readfirstlane and scalar arithmetic
+      i = (int)((uint32_t)g & 255u);
     }
     {  // the last step's book-keeping (the sink leaves `remaining`)
       const bool isW = pos == pstar, isM = pos == last;
@@ -1183,7 +1186,8 @@ struct TileU16Loader {  // twins: uint16 entries (twin_entry), row stride RS ele
   int RS;
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint16_t *p = tile + (size_t)i * RS + w * (WAVE * K) + lane;
+    // (i < 256, RS < 2^24: a 24-bit multiply, full rate, where i comes from a VGPR)
+    const uint16_t *p = tile + __umul24((uint32_t)i, (uint32_t)RS) + w * (WAVE * K) + lane;
 #pragma unroll
     for (int k = 0; k < K; ++k)  // (lanes past n read any entry: any value, never used)
       c[k] = twin_entry_cost<SH>(p[k * WAVE], E32);
