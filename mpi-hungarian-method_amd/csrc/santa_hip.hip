@@ -4783,7 +4783,6 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         nrem = __builtin_amdgcn_readfirstlane(nrem);
         par = __builtin_amdgcn_readfirstlane(par);
         minVal = __builtin_amdgcn_readfirstlane(minVal);
-        ui = __builtin_amdgcn_readfirstlane(ui);
         chT0 = __builtin_amdgcn_readfirstlane(chT0);
         chT1 = __builtin_amdgcn_readfirstlane(chT1);
         lastSel = __builtin_amdgcn_readfirstlane(lastSel);
@@ -4952,9 +4951,12 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
             __syncthreads();
           }
 #endif
+          // (the table from the word's VGPR copy: the reads' addresses and the
+          // row's u stay in VGPRs, no readfirstlane on the step's chain)
+          const uint32_t tbv = (uint32_t)g & 31u;
 #pragma unroll
-          for (int k = 0; k < K; ++k) c[k] = tbl[tb * TS + ct[k]];
-          ui = __builtin_amdgcn_readfirstlane(tbl32[tb * (TS >> 1) + TU]);
+          for (int k = 0; k < K; ++k) c[k] = tbl[tbv * TS + ct[k]];
+          ui = tbl32[tbv * (TS >> 1) + TU];
         }
         // book-keeping, one lane each in the owner wave: the winner leaves
         // `remaining`, the column at position `last` takes position pstar (its
@@ -4992,7 +4994,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
           sink = gcol;
           break;
         }
-        if constexpr (TIMED) asm volatile("" ::"v"(c[0]), "s"(ui));
+        if constexpr (TIMED) asm volatile("" ::"v"(c[0]), "v"(ui));
         stamp(4);
       }
       stamp(4);
