@@ -824,14 +824,20 @@ __device__ __forceinline__ bool sap_solve_mw_sc(const int n, const Loader &ld, c
             : "s"(st), "s"(wbase), "v"(tid8), "v"(ones)
             : "memory", "scc");
       }
-      const uint32_t ghi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(g >> 32));
+      // the decode: what the next step's VALU reads (minVal, the position
+      // pstar that leaves `remaining`, the mover's flip kX, the next row) is
+      // formed in VGPRs from the word's copy; the scalar copy of its low half
+      // serves only the loop exit and the sink
       uint32_t glo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)g);
       asm volatile("" : "+s"(glo));
-      minVal = (int64_t)((((uint64_t)ghi << 32) | (glo & ~SC_TIE_MASK)) - SC_BIAS);
+      minVal = (int64_t)((g & ~(uint64_t)SC_TIE_MASK) - SC_BIAS);
       const bool assigned = (glo >> 16) & 1u;
-      const int pk = (int)((glo >> 8) & 255u);
       const int aux = (int)(glo & 255u);
-      pstar = assigned ? pk : 255 - pk;
+      {
+        const uint32_t gv = (uint32_t)g;
+        const int pk = (int)((gv >> 8) & 255u);
+        pstar = ((gv >> 16) & 1u) ? pk : 255 - pk;
+      }
       last = nrem - 1;
       kX = (uint32_t)(last ^ pstar) << 8;
       --nrem;
