@@ -190,19 +190,26 @@ def whole_node_cpu(cb: dict, cpu: dict) -> dict:
     pool rules size worker pools to that share, so the whole node is not
     timed; blocks of a round are independent (no communication inside a
     solve), so linear scaling is an upper bound for the CPU -- it flatters
-    the CPU, never the GPU."""
+    the CPU, never the GPU.  A round's blocks are its only parallelism (each
+    waits for the previous round's state): with fewer blocks than threads
+    (78 twins blocks, 6 at 3000 pairs) at most `round_blocks` threads work, so
+    both the measured and the projected thread counts are capped there."""
     used = max(int(cb.get("cores") or cpu.get("used") or 1), 1)
     node = max(int(cpu.get("nproc") or used), used)
-    per = node / used
-    out = {"kind": "projected", "cores": node, "from_cores": used, "factor": round(per, 3),
+    nb = int(cb.get("round_blocks") or node)
+    busy, node_busy = min(used, nb), min(node, nb)
+    per = node_busy / busy
+    out = {"kind": "projected", "cores": node_busy, "from_cores": busy, "factor": round(per, 3),
+           "round_blocks": nb,
            "port_blocks_per_s": round(cb.get("value", 0.0) * per, 1),
            "reference_lap_blocks_per_s": round(cb.get("reference_lap_blocks_per_s", 0.0) * per, 1),
-           "note": f"measured on {used} leased threads x {node}/{used}: linear scaling of independent "
-                   "blocks, an upper bound for the CPU"}
+           "note": f"measured on {used} leased threads ({busy} busy) x {node_busy}/{busy}: linear "
+                   f"scaling of independent blocks over min(host threads {node}, blocks per round "
+                   f"{nb}), an upper bound for the CPU"}
     b1 = cb.get("b1_blocks_per_s") or {}
     if b1:
         p = max(b1, key=int)  # the largest P measured
-        out["b1_blocks_per_s"] = round(b1[p] * node / int(p), 2)
+        out["b1_blocks_per_s"] = round(b1[p] * node_busy / int(p), 2)
         out["b1_from_procs"] = int(p)
     return out
 
@@ -260,6 +267,7 @@ def cpu_baseline(sd, mode: int, n: int, seconds: float, cores: int):
     sc_bps, sc_done, sc_el = scipy_baseline(sd, mode, n, min(6.0, seconds / 2), cores, rows, lo, count,
                                             stride, nb)
     return {"value": round(bpsN, 2), "unit": "blocks/s", "cores": cores, "kind": "port",
+            "round_blocks": nb,
             "sample": f"{doneN} blocks (n={n}, rounds of {nb}) through oracle.round_blocks "
                       f"on {cores} threads in {elN:.1f}s; {done1} blocks on 1 core in {el1:.1f}s; "
                       f"full rescore {score_s:.2f}s per round (1 core)",

@@ -201,7 +201,12 @@ int sh_solve_blocks(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B,
  *           sh_publish_delta after the round; d_delta required).  Designs
  *           whose last launch is the fallback register-tile launch fold it
  *           into that launch's last workgroup.
- * The fallback launches of a design neither record nor sample.            */
+ * The fallback launches of a design neither record nor sample.
+ * Buffers: next_rows must not overlap d_rows or d_types, and d_undo must not
+ * overlap d_rows, d_types or next_rows (a workgroup writes them while others
+ * still read this round's rows and types): SH_ERR_ARGS.  A row out of range
+ * gets the undo entry -1, which sh_unpack_types skips (as it skips d_rows
+ * entries < 0).                                                             */
 typedef struct {
   int16_t *d_undo;
   int32_t *next_rows;
@@ -274,7 +279,8 @@ int sh_ctx_fallback_steps(sh_ctx *ctx, void *stream);
  *   sh_pack_types:   d_out[k]        = d_types[d_rows[k]]        k < count
  *   sh_unpack_types: d_types[d_rows[k] + m] = d_in[k] for m <= mode (twins:
  *                    also d_rows[k]+1; triplets: +1 and +2)
- * rows < 0 are skipped (padding).
+ * rows < 0 are skipped (padding), and so are values d_in[k] < 0 (an unpack
+ * of a padding slot, or of an undo entry of a row out of range).
  * ------------------------------------------------------------------------ */
 int sh_pack_types(const int16_t *d_types, const int32_t *d_rows, int count,
                   int16_t *d_out, void *stream);

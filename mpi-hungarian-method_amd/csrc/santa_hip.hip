@@ -20,38 +20,11 @@
 #include "santa_hip.h"
 #include "sh_common.h"
 
-// Build-time A/B switches (round 5; santa_lb_kernel: profiles/r05f_lb_ab.jsonl): prefetching each wave's
-// second-best candidate row doubled the synchronous loads' latency (640 ->
-// 1,270 cycles for a lone block) and lost 25-38 %; the one-line packed rows
-// lost 6-7 % to the int16 rows (four loads and a decode per gift pair)
-#ifndef LB_PREFETCH
-#define LB_PREFETCH 0
-#endif
-#ifndef SP3_MASKED_DUAL
-#define SP3_MASKED_DUAL 1  // santa_sp3_kernel's dual update: the visited columns only (exec-masked)
-#endif
-#ifndef LB_PACKED
-#define LB_PACKED 0
-#endif
-// santa_lb_kernel, LB_DEFER: a wave's candidate row that is not staged is
-// loaded without a wait and written after the fold only if that wave won
-// (else at the next step's top), one more barrier on those steps: the
-// winner's row was such a load on 56 % of the steps (any wave's on 80 %,
-// tools/analysis/lb_stage_sim2.py), and it lost 4-7 % (profiles/r05s_lb_defer_ab.jsonl)
-#ifndef LB_DEFER
-#define LB_DEFER 0
-#endif
+// (Variants measured and not kept are in git history and DESIGN.md, with
+// their A/B records under profiles/; the only build switch left selects the
+// santa_lb_kernel shape for 1024 < n <= 2048.)
 #ifndef LB_CFG_2048
 #define LB_CFG_2048 0  // 1024 < n <= 2048: 0 = 8 waves x 4 columns, 1 = 4 x 8, 2 = 16 x 2
-#endif
-// santa_big_kernel, each wave loading its candidate's wishlist rows before the
-// fold (the winner's row then comes from LDS): 3000-pair twins lost 22 %
-// (4,064 -> 4,978 cycles per lone step, profiles/r05o_big_staged_ab.jsonl):
-// the step is bound by its 64-bit relaxation's VALU issue (16 waves on 4
-// SIMDs), not by the row's L2 hit, and staging adds a wave DPP minimum, the
-// loads and a barrier
-#ifndef BIG_STAGED
-#define BIG_STAGED 0
 #endif
 
 namespace {
@@ -472,22 +445,6 @@ __device__ __forceinline__ uint64_t block_min_u64_rot(uint64_t wmin, uint64_t *s
   }
 }
 
-// Loaders with STAGED = true (WishRowLoader) let sap_solve_mw take the next
-// row's global load off the step's critical path: before the fold, every
-// wave issues the loads of its own candidate's row (prefetch, into
-// registers); the fold's winner is always one of the wave candidates, so
-// after the barrier the winning wave scatters the row it already holds
-// (scatter) and the next step only reads (read).  The first step of a
-// Dijkstra and a step decided by the exact argmin load as before (load).
-template <class L, class = void>
-struct staged_loader : std::false_type {};
-template <class L>
-struct staged_loader<L, std::void_t<decltype(L::STAGED)>> : std::bool_constant<L::STAGED> {};
-template <class L, bool S>
-struct staged_regs { static constexpr int value = 1; };
-template <class L>
-struct staged_regs<L, true> { static constexpr int value = L::PF; };
-
 template <int NW, int K, typename Loader, int FB = 10, typename... LA>
 __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, int64_t &steps_out,
                              int &fallbacks, const bool exact, const LA &...la) {
@@ -514,13 +471,9 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
   };
   int64_t steps = 0;
   int par = 0;  // rotating step-argmin word (0..2)
-  constexpr bool STG = staged_loader<Loader>::value && NW > 1;
-  int pf[staged_regs<Loader, STG>::value];  // (STG) the wave candidate's row, loaded before the fold
-  bool staged = false;           // (STG) this step's row was scattered by the last step's winner
   if (NW > 1 && tid < 3) S.red[tid] = ~0ull;
   __syncthreads();
   for (int cur = 0; cur < n; ++cur) {
-    staged = false;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int j = w * (WAVE * K) + k * WAVE + lane;
@@ -537,14 +490,7 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
       ++steps;
       const int64_t ui = S.u[i];
       int64_t c[K];
-      if constexpr (STG) {
-        if (staged)
-          ld.read_staged(c);
-        else
-          ld.load(i, c);
-      } else {
-        ld.load(i, c, la...);
-      }
+      ld.load(i, c, la...);
       if (NW > 1 && tid == 0) S.red[par == 2 ? 0 : par + 1] = ~0ull;
       const int64_t kU = minVal - ui;
       const uint64_t kb = (uint64_t)BIAS - (uint64_t)minVal;
@@ -570,19 +516,8 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
         best = (act && key < best) ? key : best;
       }
       uint64_t g;
-      uint64_t wm = ~0ull;  // (STG) this wave's candidate
       if constexpr (NW == 1) {
         g = wave_min_u64_fast<true>(best);
-      } else if constexpr (STG) {
-        // the wave's minimum; an assigned candidate's row loads while the
-        // fold's atomic and barrier run
-        wm = wave_min_u64_fast<true>(best);
-        const uint32_t wl = (uint32_t)wm;
-        if (wm != ~0ull && ((wl >> (2 * FB)) & 1u)) ld.prefetch((int)(wl & FM), pf);
-        if (lane == 0 && wm != ~0ull)
-          __hip_atomic_fetch_min(S.red + par, wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __syncthreads();
-        g = S.red[par];
       } else {
         // DPP min of the high words within each 16-lane row; the lanes holding
         // it (usually one per row) fold their full keys into the step word
@@ -639,11 +574,6 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
         break;
       }
       i = aux;
-      if constexpr (STG) {
-        // (an exact step's winner need not be any wave's candidate)
-        staged = !exact_step;
-        if (staged && g == wm) ld.scatter(i, pf);
-      }
     }
     // Dual update (scipy: u[cur] += minVal; u[i] += minVal - spc[col4row[i]]
     // for the other visited rows; v[j] -= minVal - spc[j] for visited cols)
@@ -1301,7 +1231,9 @@ __device__ __forceinline__ void round_prologue(const SantaArgs &a, const int b, 
   if (a.undo) {
     for (int j = (int)threadIdx.x; j < a.n; j += (int)blockDim.x) {
       const int r = a.rows[(size_t)b * a.n + j];
-      if (r >= 0 && r + mode < a.nc) a.undo[(size_t)b * a.n + j] = a.types[r];
+      // (a row out of range -- the block is refused and flagged -- gets the
+      //  sentinel -1, which unpack_kernel skips: its undo writes nothing)
+      a.undo[(size_t)b * a.n + j] = (r >= 0 && r + mode < a.nc) ? a.types[r] : (int16_t)-1;
     }
   }
   if (a.nx_rows) {
@@ -3173,6 +3105,7 @@ struct Sp3LdsRecord {
   int16_t ctype[256];         // column gift types (old)
   uint8_t own[256];           // code(i, i): row i's own gift
   uint32_t rem[512];          // scipy's `remaining`, then the rows by step (see the solve)
+  uint32_t lol[256 + 4];      // the columns' tie bits (lo) + a dump word (see the solve)
 };
 // Fused design (FUSED = true, round 4): the wave builds its own tile, so no
 // record travels through HBM (santa_tile_kernel wrote ~67 MB per round and
@@ -3191,6 +3124,7 @@ struct Sp3LdsFused {
       int32_t rowc[256 + 32];
       int32_t u_l[256 + 64];
       uint32_t rem[512];
+      uint32_t lol[256 + 4];       // the columns' tie bits (lo) + a dump word
     } s;                           // solve
     struct {
       uint32_t thead[SP4_MAX_NG];  // counting-sort counters, then the type table
@@ -3201,6 +3135,19 @@ struct Sp3LdsFused {
     } b;                           // build
   } u;
 };
+
+// The step's book-keeping (the winner leaves `remaining`, the mover takes its
+// position) changes one column's tie bits: one slot of one lane's four.  The
+// one-wave solvers keep those bits in LDS (lol[j], column j; lol[256] a dump
+// word), write the two changed words with plain DS ops in the next step's LDS
+// group and read the lane's four words back in the same group (in-order LDS:
+// the read sees the writes).  Round 5 updated a register tuple through GPR
+// index mode (s_set_gpr_idx_on) instead; with the tuple pinned to the right
+// registers it still corrupted values of other blocks at random whenever the
+// register allocation changed (VALU results of the other waves of the SIMD
+// written to the wrong register), so no kernel uses GPR indexing
+// or M0-relative moves in inline asm (tests/test_asm_lint_cpu.py).
+constexpr int SP3_LOL_OFF = 512 * 4;  // byte offset of lol from rem (the DS ops' immediate offset)
 
 template <bool TIMED, bool FUSED>
 __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const unsigned char *rec_all) {
@@ -3213,10 +3160,12 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
     rowc = SM.u.s.rowc;
     u_l = SM.u.s.u_l;
     rem = SM.u.s.rem;
+    static_assert(offsetof(Sp3LdsFused, u.s.lol) - offsetof(Sp3LdsFused, u.s.rem) == SP3_LOL_OFF, "lol after rem");
   } else {
     rowc = SM.rowc;
     u_l = SM.u_l;
     rem = SM.rem;
+    static_assert(offsetof(Sp3LdsRecord, lol) - offsetof(Sp3LdsRecord, rem) == SP3_LOL_OFF, "lol after rem");
   }
   auto ovfr = SM.ovfr;
   auto ovf = SM.ovf;
@@ -3503,10 +3452,11 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   //        is the row of step t (rowq, below); ~0: not reached
   //   W    -v_V (the range check, the outputs), Wp = W << SP3_SH (relaxation)
   //   lo   key tie-break bits (class << 10 | pkey << 2 | k); ~0: left
-  //        `remaining` this Dijkstra (or j >= n)
+  //        `remaining` this Dijkstra (or j >= n); held in LDS (lol) and read
+  //        back by every step's LDS group
   uint32_t sbp[4];
   int32_t W[4], Wp[4];
-  u32x4 lo;            // (one VGPR tuple: a step's book-keeping writes lo[k] by an indexed move)
+  u32x4 lo;
   uint32_t c4r = ~0u;  // column of row 4*lane + k in byte k
   uint32_t r4c = 0;    // row of column 4*lane + k in byte k (valid where assigned)
   // the tie bits of column j = 4 lane + k at a Dijkstra's start (pos = n-1-j):
@@ -3514,7 +3464,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   // with P = pos << 2 | k (255 - pos = pos ^ 255), kept as a table LI that
   // flips by 0x7FC for the one column a Dijkstra assigns (its sink; a column,
   // once assigned, stays so); a column j >= n (never assigned) holds ~0
-  u32x4 LI;  // (one VGPR tuple: the sink's flip is an indexed move)
+  u32x4 LI;
   // `remaining` at a Dijkstra's start: rem[p] = n - 1 - p for this lane's p
   uint4 rem0;
 #pragma unroll
@@ -3525,6 +3475,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
     LI[k] = j < n ? (((uint32_t)(n - 1 - j) << 2) | (uint32_t)k) ^ 0x3FCu : ~0u;
   }
   rem0 = make_uint4(n - 1 - 4 * lane, n - 2 - 4 * lane, n - 3 - 4 * lane, n - 4 - 4 * lane);
+  const uint32_t m1 = ~0u;  // (the winner's tie bits: the DS write's data VGPR)
   // rem[p]: the column at position p of scipy's `remaining`; rowq[n - 1 - t]:
   // the LDS address of u_l[i] for the row i of step t (written by the step's
   // LDS group from the address it reads the dual with)
@@ -3558,24 +3509,27 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       // Dijkstra set-up: remaining = [n-1 .. 0], every column < n live, spc = inf
       int ln = lane;
       asm volatile("" : "+v"(ln));
-      lo = LI;
 #pragma unroll
       for (int k = 0; k < 4; ++k) sbp[k] = ~0u;
+      // (rem + 16 lane: this lane's `remaining` words, and at +SP3_LOL_OFF
+      //  its four tie-bit words, lol[4 lane ..] = LI)
+      const uint32_t r16 = lds_addr(rem) + 16u * (uint32_t)ln;
       *(uint4 *)(rem + 4 * ln) = rem0;
+      *(uint4 *)(rem + 4 * ln + SP3_LOL_OFF / 4) = make_uint4(LI[0], LI[1], LI[2], LI[3]);
       int nrem = n;
       uint32_t rq = lds_addr(rem) + 4u * (uint32_t)(n - 1);  // &rem[nrem - 1], stepped down
       asm volatile("" : "+v"(rq));  // (a VGPR: the LDS address operand, stepped by one VALU)
       uint32_t mvb = (uint32_t)SP3_BIAS;  // minVal + BIAS (the key's value field of the last winner)
       int i = cur;
       int sink;
-      // deferred book-keeping of the previous step, applied in the shadow of
-      // the next step's LDS group: the winner (lane, slot) leaves `remaining`
-      // (lo = ~0), the mover (the column at the last position) takes the
-      // winner's position (its pkey bits ^= kX); a lane mask of 0: none
-      uint64_t wmask = 0, mmask = 0;
-      int kw = 0, kmv = 0;
-      uint32_t kX = 0;  // (a VGPR: the xor's vector operand)
-      asm volatile("" : "+v"(kX));
+      // deferred book-keeping of the previous step, applied by the next
+      // step's LDS group: the winner leaves `remaining` (lol[winner] = ~0),
+      // the mover (the column at the last position) takes the winner's
+      // position (lol[mover] ^= kX); both addresses rem + 4 j (+ SP3_LOL_OFF
+      // in the DS op); the first step of a Dijkstra writes the dump word
+      uint32_t wa = lds_addr(rem) + 4u * 256u, ma = wa;
+      uint32_t kX = 0;  // (a VGPR: the xor's data)
+      asm volatile("" : "+v"(kX), "+v"(wa), "+v"(ma));
       bool first = true;
       for (;;) {
         ++steps;
@@ -3608,44 +3562,42 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         int2 c01, c23;
         // The step's LDS traffic as one issue group for every row (a row with
         // more than 32 hits has the marker, whose slot is a dump slot, in its
-        // entry 31; such a row re-reads its columns below): the dual and the
-        // mover, the scatter, the row reads (two ds_read_b64 of slots 2l, 2l+1
-        // and 128+2l, 129+2l: one bank per lane of a 32-lane group, where the
-        // ds_read2_b32 pairs were 2-way on both halves), the un-scatter, the step's row
-        // (rowq[nrem - 1] = the dual's address) -- no wait in between; then
-        // the previous step's book-keeping in their shadow, one lane and one
-        // register each (a v_cndmask on that lane's mask, the slot by GPR
-        // indexing on the lo tuple, %17 = its first register; no exec
-        // changes: four SALU fewer), one wait at the end.  Operands stay
-        // live through that wait.  (The one-word stores by all 64 lanes --
-        // this rowq entry, rem[pstar] after the decode -- measured 5 % faster
-        // per lone step than the same stores by one lane under an exec mask:
-        // profiles/r04_ab_stores.jsonl.)
+        // entry 31; such a row re-reads its columns below): the previous
+        // step's book-keeping (the winner's tie-bit word written by every
+        // lane, the mover's xor by lane 0: an atomic by 64 lanes would
+        // serialise), the dual and the mover, the scatter, the row reads (two
+        // ds_read_b64 of slots 2l, 2l+1 and 128+2l, 129+2l: one bank per lane
+        // of a 32-lane group, where the ds_read2_b32 pairs were 2-way on both
+        // halves), this lane's four tie-bit words, the un-scatter, the step's
+        // row (rowq[nrem - 1] = the dual's address) -- no wait in between,
+        // one wait at the end.  Operands stay live through that wait.  (The
+        // one-word stores by all 64 lanes -- this rowq entry, rem[pstar] after
+        // the decode -- measured 5 % faster per lone step than the same stores
+        // by one lane under an exec mask: profiles/r04_ab_stores.jsonl.)
         uint32_t ua;  // (u_l + 4 i formed by one VALU: the address is a VGPR operand anyway)
         asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(ua) : "s"(i), "v"(ubv));
         const uint32_t ra = rq;
         const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
         const int32_t miss = SP3_MISS;
-        uint32_t sv;  // (the mover's xor term: kX in its lane, 0 elsewhere)
+        uint64_t sv;  // (exec, saved around the mover's one-lane xor)
         asm volatile(
+            "ds_write_b32 %12, %14 offset:%c17\n\t"
+            "s_mov_b64 %5, exec\n\t"
+            "s_mov_b64 exec, 1\n\t"
+            "ds_xor_b32 %13, %15 offset:%c17\n\t"
+            "s_mov_b64 exec, %5\n\t"
             "ds_read_b32 %0, %6\n\t"
             "ds_read_b32 %1, %7\n\t"
             "ds_write_b32 %8, %9\n\t"
             "ds_read_b64 %2, %10\n\t"
             "ds_read_b64 %3, %10 offset:512\n\t"
+            "ds_read_b128 %4, %16 offset:%c17\n\t"
             "ds_write_b32 %8, %11\n\t"
             "ds_write_b32 %7, %6 offset:1024\n\t"
-            "v_cndmask_b32 %4, 0, %16, %14\n\t"
-            "s_set_gpr_idx_on %13, gpr_idx(SRC0,DST)\n\t"
-            "v_cndmask_b32 %17, %17, -1, %12\n\t"
-            "s_set_gpr_idx_off\n\t"
-            "s_set_gpr_idx_on %15, gpr_idx(SRC1,DST)\n\t"
-            "v_xor_b32 %17, %4, %17\n\t"
-            "s_set_gpr_idx_off\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "=&v"(sv), "+v"(lo)
-            : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(miss), "s"(wmask), "s"(kw), "s"(mmask),
-              "s"(kmv), "v"(kX), "v"(lo.x)
+            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "=&v"(lo), "=&s"(sv)
+            : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(miss), "v"(wa), "v"(ma), "v"(m1),
+              "v"(kX), "v"(r16), "i"(SP3_LOL_OFF)
             : "memory");
         // (a row with more than 32 hits: the tile's entries and the overflow
         // list scattered again, the four columns re-read; the other half's
@@ -3699,17 +3651,17 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           stamp(tB);
         }
         mvb = g >> SP3_SH;
-        kw = (int)(g & 3u);
+        const int kw = (int)(g & 3u);
         const uint32_t pkey = (g >> 2) & 255u;
         const bool assigned = (g >> 10) & 1u;
         const int lw = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == g));
         const int pstar = assigned ? (int)pkey : 255 - (int)pkey;
         const int last = nrem - 1;
         asm("v_lshlrev_b32 %0, 2, %1" : "=v"(kX) : "s"(last ^ pstar));
-        wmask = 1ull << lw;
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
-        mmask = 1ull << (mv >> 2);
-        kmv = mv & 3;
+        // (the next group's book-keeping addresses: rem + 4 j of the winner and the mover)
+        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(wa) : "s"(4 * lw + kw), "v"(remv));
+        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(ma) : "s"(mv), "v"(remv));
         {  // rem[pstar] = mover (every lane, same word; a no-op when pstar == last)
           uint32_t pa;
           asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(pa) : "s"(pstar), "v"(remv));
@@ -3730,9 +3682,9 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       // column's path row: the row of the step in sbp's low byte (rowq; an
       // unreached column reads an unused in-bounds word).
       const int32_t minVal = (int32_t)mvb - SP3_BIAS;
-      i32x4 prow;  // (one VGPR tuple: the augmentation selects prow[j & 3] by an indexed move)
-#if SP3_MASKED_DUAL  // (the visited columns and the sink only; 1 % faster here,
-                     //  2-4 % slower in santa_dt_kernel: profiles/r05h_masked_dual_ab.jsonl)
+      int32_t prow[4];
+      // (the visited columns and the sink only, exec-masked: DESIGN §4.0b; 1 % faster
+      //  here, 2-4 % slower in santa_dt_kernel: profiles/r05h_masked_dual_ab.jsonl)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const bool vk = (lo[k] == ~0u || 4 * lane + k == sink) && (4 * lane + k < n);
@@ -3745,32 +3697,12 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         }
         accW |= (uint32_t)W[k] + LR.CW;
       }
-#else
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
-        const int32_t dd = vk ? (int32_t)(mvb - (sbp[k] >> SP3_SH)) : 0;
-        W[k] += dd;
-        Wp[k] = (int32_t)((uint32_t)W[k] << SP3_SH);
-        accW |= (uint32_t)W[k] + LR.CW;
-        const int ua = vk ? (int)((r4c >> (8 * k)) & 0xFFu) : 256 + lane;
-        __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
-      }
-#endif
       if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      // the sink is the one column this Dijkstra assigns
       {  // the sink is the one column this Dijkstra assigns: flip its start tie bits
-        uint64_t sv;
-        asm volatile(
-            "s_mov_b64 %1, exec\n\t"
-            "s_mov_b64 exec, %2\n\t"
-            "s_set_gpr_idx_on %3, gpr_idx(SRC1,DST)\n\t"
-            "v_xor_b32 %4, 0x7fc, %4\n\t"
-            "s_set_gpr_idx_off\n\t"
-            "s_mov_b64 exec, %1"
-            : "+v"(LI), "=&s"(sv)
-            : "s"(1ull << (sink >> 2)), "s"(sink & 3), "v"(LI.x));
+        const int sk = sink & 3;
+        const bool sl = lane == (sink >> 2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) LI[k] ^= (sl && k == sk) ? 0x7FCu : 0u;
       }
       stamp(tD1);
       // augment along the path from the sink back to cur (registers only; at
@@ -3780,13 +3712,8 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       int j = sink, pi = -1, left = n;
       do {
         const int jl = j >> 2;
-        int pv;  // prow[j & 3] (one indexed move), then lane jl of it
-        asm volatile(
-            "s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\t"
-            "v_mov_b32 %0, %2\n\t"
-            "s_set_gpr_idx_off"
-            : "=v"(pv)
-            : "s"(j & 3), "v"(prow.x), "v"(prow));
+        const int jk = j & 3;  // prow[j & 3] (uniform selects), then lane jl of it
+        const int pv = jk == 0 ? prow[0] : jk == 1 ? prow[1] : jk == 2 ? prow[2] : prow[3];
         const int pa = __builtin_amdgcn_readlane(pv, jl);
         pi = (int)(((uint32_t)pa - ubase) >> 2);
         // row pi: its previous column t leaves, j becomes its column
@@ -3808,12 +3735,16 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   }
   stamp(tD);
   __syncthreads();
+  // (the lane index re-read for the tail: the prologue's 4 lane + k compares
+  //  are not kept live across the solve, where every VGPR is taken)
+  int lq = lane;
+  asm volatile("" : "+v"(lq));
 
   {  // the lattice range (see above): leave the block to the fallback launch
     bool big = bad || ((accU & LR.MU) | (accW & LR.MW)) != 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k)  // (the output decode's u)
-      if (4 * lane + k < n) big |= (((uint32_t)u_l[4 * lane + k] + LR.CU) & LR.MU) != 0;
+      if (4 * lq + k < n) big |= (((uint32_t)u_l[4 * lq + k] + LR.CU) & LR.MU) != 0;
     if (__builtin_expect(__any(big), 0)) {
       if (lane == 0) {
         const int p = atomicAdd(a.ovf_cnt, 1);
@@ -3826,7 +3757,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   int64_t cost = 0, dch = 0, dgh = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int i = 4 * lane + k;
+    const int i = 4 * lq + k;
     const int col = (int)((c4r >> (8 * k)) & 0xFFu);
     int32_t vq[4];
 #pragma unroll
@@ -3909,6 +3840,7 @@ __host__ __device__ __forceinline__ DtLds dt_lds_layout(int n, int ng) {
   L.rows = off;  off += r16((size_t)n * 4);
   L.ctype = off; off += r16((size_t)n * 2);
   L.rem = off;   off += 512 * 4;         // `remaining`, then the rows by step (santa_sp3_kernel)
+  off += (256 + 4) * 4;                  // the columns' tie bits at rem + SP3_LOL_OFF (santa_sp3_kernel)
   L.head = off;  off += r16((size_t)ng * 4);
   L.nxt = off;   off += r16((size_t)n * 2);
   L.total = off;
@@ -3959,14 +3891,14 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
   const uint32_t MK = (uint32_t)SP3_MISS + ((uint32_t)nw1 << 20);
   uint32_t sbp[4];
   int32_t W[4], Wp[4];
-  u32x4 lo;
+  u32x4 lo;  // (read from LDS by every step's group, as in santa_sp3_kernel)
   uint32_t c4r = ~0u, r4c = 0;
   // the tie bits of column j = 4 lane + k at a Dijkstra's start (pos = n-1-j):
   // (assigned ? 256 | pos : 255 - pos) << 2 | k, i.e. P ^ 0x400 or P ^ 0x3FC
   // with P = pos << 2 | k (255 - pos = pos ^ 255), kept as a table LI that
   // flips by 0x7FC for the one column a Dijkstra assigns (its sink; a column,
   // once assigned, stays so); a column j >= n (never assigned) holds ~0
-  u32x4 LI;  // (one VGPR tuple: the sink's flip is an indexed move)
+  u32x4 LI;
   // `remaining` at a Dijkstra's start: rem[p] = n - 1 - p for this lane's p
   uint4 rem0;
 #pragma unroll
@@ -3980,6 +3912,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
   uint32_t *rowq = rem + 256;
   const uint32_t ubase = lds_addr(u_l);
   const uint32_t tbase = lds_addr(tile8) + 4u * (uint32_t)lane;
+  const uint32_t m1 = ~0u;  // (the winner's tie bits: the DS write's data VGPR)
   int steps = 0;
   bool bad = (a.flags & (SH_FLAG_TEST_RANGE | SH_FLAG_EXACT_ARGMIN)) != 0 || !LR.ok;
   uint32_t accU = 0, accW = 0;
@@ -3992,18 +3925,18 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       if (cur == n - SP3_PRIO_C) __builtin_amdgcn_s_setprio(0);
       int ln = lane;
       asm volatile("" : "+v"(ln));
-      lo = LI;
 #pragma unroll
       for (int k = 0; k < 4; ++k) sbp[k] = ~0u;
+      const uint32_t r16 = lds_addr(rem) + 16u * (uint32_t)ln;  // (+ SP3_LOL_OFF: this lane's tie bits)
       *(uint4 *)(rem + 4 * ln) = rem0;
+      *(uint4 *)(rem + 4 * ln + SP3_LOL_OFF / 4) = make_uint4(LI[0], LI[1], LI[2], LI[3]);
       if (lane == 0) rowq[n - 1] = ubase + 4u * (uint32_t)cur;  // (step 0's row)
       int nrem = n;
       int32_t minVal = 0;
       int i = cur;
       int sink;
-      uint64_t wmask = 0, mmask = 0;
-      int kw = 0, kmv = 0;
-      uint32_t kX = 0;
+      uint64_t wmask = 0;  // the previous winner's lane: its one-lane stores (none on step 0)
+      uint32_t kX = 0, wa = 0, ma = 0;  // the previous step's mover xor and the two tie-bit words
       uint32_t rpa = 0;   // the previous step's rem[pstar] address
       int mover_v = 0;    // its mover, stored by the group, then replaced by this step's
       for (;;) {
@@ -4015,34 +3948,29 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         const uint32_t ta = tbase + (uint32_t)i * DT_RS;
         uint64_t sv;
         // the step's LDS group (santa_sp3_kernel's, with the tile row read
-        // in place of the scatter / row reads / un-scatter), the previous
-        // step's book-keeping in its shadow, one wait.  Here the one-word
-        // stores (the previous step's rem[pstar] = mover, this step's rowq
-        // entry) go by one lane (exec = the previous winner's lane; none on a
-        // Dijkstra's first step, whose row the set-up stores): 2 % faster per
-        // lone step than by all 64 lanes, the reverse of santa_sp3_kernel
+        // in place of the scatter / row reads / un-scatter), one wait.  Here
+        // the one-word stores (the previous step's rem[pstar] = mover, this
+        // step's rowq entry, the previous step's two tie-bit words) go by one
+        // lane (exec = the previous winner's lane; none on a Dijkstra's first
+        // step, whose row the set-up stores): 2 % faster per lone step than
+        // by all 64 lanes, the reverse of santa_sp3_kernel
         // (profiles/r04_ab_dt_stores.jsonl, r04_ab_stores.jsonl)
         asm volatile(
             "s_mov_b64 %3, exec\n\t"
-            "s_mov_b64 exec, %9\n\t"
-            "ds_write_b32 %14, %1\n\t"
+            "s_mov_b64 exec, %8\n\t"
+            "ds_write_b32 %9, %1\n\t"
             "ds_write_b32 %6, %5 offset:1024\n\t"
+            "ds_write_b32 %10, %12 offset:%c15\n\t"
+            "ds_xor_b32 %11, %13 offset:%c15\n\t"
             "s_mov_b64 exec, %3\n\t"
             "ds_read_b32 %2, %7\n\t"
             "ds_read_b32 %0, %5\n\t"
             "ds_read_b32 %1, %6\n\t"
-            "s_mov_b64 exec, %9\n\t"
-            "s_set_gpr_idx_on %10, gpr_idx(DST)\n\t"
-            "v_mov_b32 %8, -1\n\t"
-            "s_set_gpr_idx_off\n\t"
-            "s_mov_b64 exec, %11\n\t"
-            "s_set_gpr_idx_on %12, gpr_idx(SRC1,DST)\n\t"
-            "v_xor_b32 %8, %13, %8\n\t"
-            "s_set_gpr_idx_off\n\t"
-            "s_mov_b64 exec, %3\n\t"
+            "ds_read_b128 %4, %14 offset:%c15\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "+v"(mover_v), "=&v"(w4), "=&s"(sv), "+v"(lo)
-            : "v"(ua), "v"(ra), "v"(ta), "v"(lo.x), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv), "s"(kX), "v"(rpa)
+            : "=&v"(uraw), "+v"(mover_v), "=&v"(w4), "=&s"(sv), "=&v"(lo)
+            : "v"(ua), "v"(ra), "v"(ta), "s"(wmask), "v"(rpa), "v"(wa), "v"(ma), "v"(m1), "v"(kX),
+              "v"(r16), "i"(SP3_LOL_OFF)
             : "memory");
         const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
         accU |= (uint32_t)ui + LR.CU;
@@ -4061,7 +3989,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         const uint32_t rsel = __builtin_amdgcn_ubfe(r4c, best << 3, 8);
         const uint32_t g = wave_min_u32_dpp(best);
         minVal = (int32_t)(g >> SP3_SH) - SP3_BIAS;
-        kw = (int)(g & 3u);
+        const int kw = (int)(g & 3u);
         const uint32_t pkey = (g >> 2) & 255u;
         const bool assigned = (g >> 10) & 1u;
         const int lw = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == g));
@@ -4070,9 +3998,9 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         kX = (uint32_t)(last ^ pstar) << 2;
         wmask = 1ull << lw;
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
-        mmask = 1ull << (mv >> 2);
-        kmv = mv & 3;
         rpa = lds_addr(rem) + 4u * (uint32_t)pstar;  // (stored by the next step's group)
+        wa = lds_addr(rem) + 4u * (uint32_t)(4 * lw + kw);  // (the winner's and the mover's tie bits)
+        ma = lds_addr(rem) + 4u * (uint32_t)mv;
         --nrem;
         sink = 4 * lw + kw;
         i = __builtin_amdgcn_readlane((int)rsel, lw);
@@ -4080,25 +4008,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       }
       // dual update, path rows, augmentation: santa_sp3_kernel's
       const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
-      i32x4 prow;
-#ifdef DT_MASKED_DUAL
-      // (dev, DESIGN §4.0b: round 4's exec-masked variant = 1, which skipped
-      // the sink's path row -- the sink's removal is deferred, so its lo is
-      // not ~0 here -- and sent every block to the fallback launch; 2 = the
-      // same with the sink included)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool vk = (lo[k] == ~0u || (DT_MASKED_DUAL == 2 && 4 * lane + k == sink)) && (4 * lane + k < n);
-        if (vk) {
-          const int32_t dd = (int32_t)(mvb - (sbp[k] >> SP3_SH));
-          W[k] += dd;
-          Wp[k] = (int32_t)((uint32_t)W[k] << SP3_SH);
-          __hip_atomic_fetch_add(u_l + ((r4c >> (8 * k)) & 0xFFu), dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
-        }
-        accW |= (uint32_t)W[k] + LR.CW;
-      }
-#else
+      int32_t prow[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
@@ -4110,30 +4020,18 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         __hip_atomic_fetch_add(u_l + ua, dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         prow[k] = (int32_t)rowq[n - 1 - (int)(sbp[k] & 0xFFu)];
       }
-#endif
       if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       {  // the sink is the one column this Dijkstra assigns: flip its start tie bits
-        uint64_t sv;
-        asm volatile(
-            "s_mov_b64 %1, exec\n\t"
-            "s_mov_b64 exec, %2\n\t"
-            "s_set_gpr_idx_on %3, gpr_idx(SRC1,DST)\n\t"
-            "v_xor_b32 %4, 0x7fc, %4\n\t"
-            "s_set_gpr_idx_off\n\t"
-            "s_mov_b64 exec, %1"
-            : "+v"(LI), "=&s"(sv)
-            : "s"(1ull << (sink >> 2)), "s"(sink & 3), "v"(LI.x));
+        const int sk = sink & 3;
+        const bool sl = lane == (sink >> 2);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) LI[k] ^= (sl && k == sk) ? 0x7FCu : 0u;
       }
       int j = sink, pi = -1;
       for (int hop = 0; hop <= n; ++hop) {
         const int jl = j >> 2;
-        int pv;
-        asm volatile(
-            "s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\t"
-            "v_mov_b32 %0, %2\n\t"
-            "s_set_gpr_idx_off"
-            : "=v"(pv)
-            : "s"(j & 3), "v"(prow.x), "v"(prow));
+        const int jk = j & 3;
+        const int pv = jk == 0 ? prow[0] : jk == 1 ? prow[1] : jk == 2 ? prow[2] : prow[3];
         const int pa = __builtin_amdgcn_readlane(pv, jl);
         pi = (int)(((uint32_t)pa - ubase) >> 2);
         const int pl = pi >> 2, ps = 8 * (pi & 3);
@@ -4215,11 +4113,8 @@ struct WishRowLoader {
   int n, nw, nw1;
   int64_t E;
   const int64_t *lut;     // twins: twin_lut_index -> exact cost (LDS), as the 4-wave twins kernel
-  int16_t *stage;         // LDS [M * nw] (STAGED): the winning wave's prefetched row
   static constexpr int M = MODE + 1;                     // children per unit
   static constexpr int BPC = MODE == 0 ? 1 : 2 * MODE;  // rowbuf bytes per column
-  static constexpr bool STAGED = BIG_STAGED != 0;
-  static constexpr int PF = 2 * M;                       // prefetch registers: ranks lane, lane + 64 per child
   static_assert(NW * WAVE >= (MODE + 1) * 127, "one thread per wish of a unit (n_wish <= 127)");
   // the code of wish rank r of member vr to every column of gift type g
   __device__ __forceinline__ void put(int g, int vr, int r) const {
@@ -4249,39 +4144,6 @@ struct WishRowLoader {
     }
     read(c);
   }
-  // (STAGED) the wave's candidate unit i: lane l loads ranks l and l + 64 of
-  // every member (-1 past n_wish); nothing waits for them here
-  __device__ __forceinline__ void prefetch(int i, int (&pf)[PF]) const {
-    const int lane = threadIdx.x & 63;
-    const uint32_t base = (uint32_t)rows[i] * (uint32_t)nw;
-#pragma unroll
-    for (int vr = 0; vr < M; ++vr) {
-      const int16_t *src = wish + base + (uint32_t)(vr * nw);
-      pf[2 * vr] = lane < nw ? src[lane] : -1;
-      pf[2 * vr + 1] = lane + WAVE < nw ? src[lane + WAVE] : -1;
-    }
-  }
-  // (STAGED) the winning wave writes the row it prefetched into the staging
-  // list (one gift per wish, as the distributed load reads them)
-  __device__ __forceinline__ void scatter(int, const int (&pf)[PF]) const {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int vr = 0; vr < M; ++vr) {
-      if (lane < nw) stage[vr * nw + lane] = (int16_t)pf[2 * vr];
-      if (lane + WAVE < nw) stage[vr * nw + lane + WAVE] = (int16_t)pf[2 * vr + 1];
-    }
-  }
-  // (STAGED) the next step's row from the staging list: every wish's type
-  // scattered by its own thread, as load() does after its global read
-  __device__ __forceinline__ void read_staged(int64_t (&c)[K]) const {
-    const int tid = threadIdx.x;
-    __syncthreads();
-    if (tid < M * nw) {
-      const int vr = tid / nw;
-      put(stage[tid], vr, tid - vr * nw);
-    }
-    read(c);
-  }
   __device__ __forceinline__ void read(int64_t (&c)[K]) const {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     __syncthreads();
@@ -4307,7 +4169,7 @@ struct WishRowLoader {
 };
 
 struct BigLds {
-  size_t u, c4r, r4c, path, red, rows, ctype, csort, thead, rowbuf, part, scan, stage, lut, total;
+  size_t u, c4r, r4c, path, red, rows, ctype, csort, thead, rowbuf, part, scan, lut, total;
 };
 
 // (the row buffer covers the NW * 64 * K columns the solver's threads own:
@@ -4327,7 +4189,6 @@ __host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int n
   L.rowbuf = o; o += r16((size_t)(nw * 64 * k) * (mode == 0 ? 1 : 2 * mode));
   L.part = o;   o += r16((size_t)nw * 3 * 8);
   L.scan = o;   o += r16((size_t)nw * 4);
-  L.stage = o;  o += r16((size_t)(mode + 1) * 128 * 2);
   L.lut = o;    o += mode == 1 ? (size_t)TWIN_LUT * 8 : 0;
   L.total = o;
   return L;
@@ -4491,8 +4352,7 @@ __device__ __forceinline__ void santa_big_block(const SantaArgs &a, const int b)
     for (int i = tid; i < n; i += WG) S.c4r[i] = (int16_t)i;
     __syncthreads();
   } else {
-    const WishRowLoader<MODE, NW, K> ld{a.wish, rows_l, thead, csort, rowbuf, n, a.n_wish, nw1, a.E, lut,
-                                        (int16_t *)(smem + L.stage)};
+    const WishRowLoader<MODE, NW, K> ld{a.wish, rows_l, thead, csort, rowbuf, n, a.n_wish, nw1, a.E, lut};
     sap_solve_mw<NW, K, WishRowLoader<MODE, NW, K>, FB>(n, ld, S, steps, fallbacks,
                                                          (a.flags & SH_FLAG_EXACT_ARGMIN) != 0);
   }
@@ -4602,7 +4462,7 @@ struct LbRange {
 // relaxation + lane minimum, 1 wave DPP minimum, 2 candidate (readlanes,
 // synchronous row staging, the fold, the next candidate's prefetch), 3
 // barrier, 4 word read + decode + the next row's reads + book-keeping, 5
-// per-Dijkstra work, 6 rows staged synchronously, 7 rows prefetched.
+// per-Dijkstra work, 6 rows staged synchronously, 7 unused (0).
 //
 // The step (wave w, columns j = (w K + k) 64 + lane):
 //   reads   c[k] = tbl[tb][type of j], u~ from the table's u entry (one LDS
@@ -4610,14 +4470,10 @@ struct LbRange {
 //   relax   r = W + c - u~ in key units, sbp = min(sbp, r << 12 | t), key
 //   argmin  lane min, wave DPP min -> the wave's candidate (lane, k by
 //           readlanes); an assigned candidate's row must be in one of the
-//           wave's two tables: usually it is (prefetched, below), else it is
-//           loaded now (the step's only dependent global load); the table's u
+//           wave's two tables: it is when the wave staged it on an earlier
+//           step, else it is loaded now (the step's only dependent global
+//           load) into the table the wave did not publish last; the table's u
 //           entry gets u[row]; ds_min_u64 of the step word
-//   prefetch the wave's second-best candidate (the best among the other
-//           lanes' minima: the winning wave's next candidate is its previous
-//           second-best ~85 % of the time, tools/analysis/lb_stage_sim.py)
-//           is loaded into registers now and written into the wave's other
-//           table at the top of the next step, when no wave reads that table
 //   barrier, decode (SGPRs), the next step's reads, then the book-keeping
 //           (the winner leaves `remaining`, the mover's tie bits) in their shadow
 template <int NW, int K, bool TIMED = false>
@@ -4704,31 +4560,18 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
     int chT0 = -1, chT1 = -1, lastSel = 0;
     const uint32_t ogd = (uint32_t)(DUMP + lane) * 0x10001u;  // (both gifts at the lane's dump entry)
     uint32_t og0 = ogd, og1 = ogd;
-    // the prefetched row (child pch, for table 2w + pZ), held in registers
-    int pch = -1, pZ = 0, pg0 = -1, pg1 = -1;
     // row cur's table 2 NW + (cur & 1): the last wave loads row cur + 1 at the
     // start of Dijkstra cur and writes it at its end
     uint32_t ogC0 = ogd, ogC1 = ogd;
     int cg0 = -1, cg1 = -1;
-    // a row's gifts: lane l holds ranks l and l + 64 (-1 past n_wish); from
-    // the packed line (gift r at bits 10 r .. 10 r + 9: one 128-byte line, one
-    // request) or the int16 row (200 bytes over two or three lines)
-    const bool packed = LB_PACKED && a.wish10 != nullptr;
+    // a row's gifts: lane l holds ranks l and l + 64 (-1 past n_wish), from
+    // the int16 row (200 bytes over two or three lines; the 10-bit packed
+    // line lost 6-7 %: four loads and a decode per gift pair,
+    // profiles/r05f_lb_ab.jsonl)
     auto load_row = [&](int child, int &g0, int &g1) {
-      if (packed) {
-        const uint32_t *line = a.wish10 + (size_t)(uint32_t)child * 32u;
-        const uint32_t b0 = 10u * (uint32_t)lane, b1 = 10u * (uint32_t)(lane + WAVE);
-        const bool v0 = lane < nw, v1 = lane + WAVE < nw;
-        const uint32_t d0 = b0 >> 5, d1 = v1 ? (b1 >> 5) : 0u;
-        const uint32_t x0 = v0 ? line[d0] : 0u, y0 = v0 ? line[min(d0 + 1u, 31u)] : 0u;
-        const uint32_t x1 = v1 ? line[d1] : 0u, y1 = v1 ? line[min(d1 + 1u, 31u)] : 0u;
-        g0 = v0 ? (int)(__builtin_amdgcn_alignbit(y0, x0, b0 & 31u) & 1023u) : -1;
-        g1 = v1 ? (int)(__builtin_amdgcn_alignbit(y1, x1, b1 & 31u) & 1023u) : -1;
-      } else {
-        const int16_t *src = a.wish + (size_t)(uint32_t)child * (uint32_t)nw;
-        g0 = lane < nw ? src[lane] : -1;
-        g1 = lane + WAVE < nw ? src[lane + WAVE] : -1;
-      }
+      const int16_t *src = a.wish + (size_t)(uint32_t)child * (uint32_t)nw;
+      g0 = lane < nw ? src[lane] : -1;
+      g1 = lane + WAVE < nw ? src[lane + WAVE] : -1;
     };
     // (a lane with no gift writes its dump entry: four stores with no exec
     // masking; one wave: its clears land before its writes)
@@ -4751,7 +4594,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
     uint32_t accU = 0, accW = 0;
     int par = 0;  // rotating step word
     uint64_t seg[6] = {0, 0, 0, 0, 0, 0}, ts = 0, ldlat = 0;
-    uint32_t nsync = 0, npre = 0, nwin = 0;
+    uint32_t nsync = 0;
     auto stamp = [&](int q) {
       if constexpr (TIMED) {
         const uint64_t x = __builtin_amdgcn_s_memtime();
@@ -4792,22 +4635,10 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         chT0 = __builtin_amdgcn_readfirstlane(chT0);
         chT1 = __builtin_amdgcn_readfirstlane(chT1);
         lastSel = __builtin_amdgcn_readfirstlane(lastSel);
-        pch = __builtin_amdgcn_readfirstlane(pch);
-        pZ = __builtin_amdgcn_readfirstlane(pZ);
         ++steps;
         if (w == 0) {  // (every lane of wave 0, same words: a scalar branch, no exec mask)
           rowq[t] = (int16_t)i;
           words[par == 2 ? 0 : par + 1] = ~0ull;  // re-arm the next step's word
-        }
-        if (pch >= 0) {  // the prefetched row into its table (no wave reads it this step)
-          if (pZ == 0) {
-            write_row(2 * w, pg0, pg1, og0);
-            chT0 = pch;
-          } else {
-            write_row(2 * w + 1, pg0, pg1, og1);
-            chT1 = pch;
-          }
-          pch = -1;
         }
         const int32_t ut = ui - minVal;
         accU |= (uint32_t)ut + R.CU;
@@ -4838,10 +4669,11 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         const uint32_t wmin = wave_min_u32_dpp(best);
         if constexpr (TIMED) asm volatile("" ::"s"(wmin));
         stamp(1);
-        // (LB_DEFER) this wave's candidate row, loaded this step without a
-        // wait: child pend (-1 none), gifts sg0/sg1, for table 2w + (slot & 1)
-        int pend = -1, sg0 = -1, sg1 = -1;
-        [[maybe_unused]] int pslot = 0;
+        // (the wave's candidate row, when it is loaded now: gifts sg0 / sg1;
+        // prefetching the wave's second-best candidate lost 25-38 % and a
+        // deferred write of the row 4-7 %: profiles/r05f_lb_ab.jsonl,
+        // r05s_lb_defer_ab.jsonl)
+        int sg0 = -1, sg1 = -1;
         if (wmin != ~0u) {
           const int wl = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == wmin));
           const int kk = __builtin_amdgcn_readlane((int)kb, wl);
@@ -4864,49 +4696,19 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
               if (2 * w + v == tb) v ^= 1;
               if constexpr (TIMED) tl = __builtin_amdgcn_s_memtime();
               load_row(ch, sg0, sg1);
-#if LB_DEFER
-              pend = ch;  // (written after the fold if this wave wins, else at the next step's top)
-#else
               if (v == 0) chT0 = ch;
               else chT1 = ch;
               sync = true;
-#endif
               ++nsync;
             }
             lastSel = v;
             slot = 2 * w + v;
-            pslot = slot;
             tbl32[slot * (TS >> 1) + TU] = uu;  // (every lane, same word)
           }
           const uint64_t word = ((uint64_t)wmin << 32) | ((uint32_t)col << 17) | ((inf & 0x7FFu) << 6) |
-                                (pend >= 0 ? 32u : 0u) | (uint32_t)slot;
+                                (uint32_t)slot;
           if (lane == 0)
             __hip_atomic_fetch_min(words + par, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if LB_PREFETCH
-          // the wave's next candidate, most likely: the best among the other
-          // lanes (computed while the synchronous load is in flight)
-          const uint32_t wmin2 = wave_min_u32_dpp(lane == wl ? ~0u : best);
-          if (wmin2 != ~0u && ((wmin2 >> 11) & 1u)) {
-            const int wl2 = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == wmin2));
-            int kk2 = K - 1;
-#pragma unroll
-            for (int k = K - 2; k >= 0; --k)
-              if ((uint32_t)__builtin_amdgcn_readlane((int)key[k], wl2) == wmin2) kk2 = k;
-            uint32_t inf2 = 0;
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-              if (k == kk2) inf2 = (uint32_t)__builtin_amdgcn_readlane((int)info[k], wl2);
-            const int ch2 = (int)(inf2 >> 11);
-            if (ch2 != chT0 && ch2 != chT1) {
-              // into the table this step did not publish (written at the top
-              // of the next step, which reads the winner's table: not this one)
-              pZ = asg ? (slot & 1) ^ 1 : lastSel ^ 1;
-              pch = ch2;
-              load_row(ch2, pg0, pg1);
-              ++npre;
-            }
-          }
-#endif
           if (sync) {  // the synchronous row into its table before the barrier
             if constexpr (TIMED) {
               asm volatile("" ::"v"(sg0), "v"(sg1));
@@ -4939,24 +4741,6 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         if (assigned) {  // the next step's row: its reads first
           i = (int)((gl >> 6) & 0x7FFu);
           tb = (int)(gl & 31u);
-#if LB_DEFER
-          // the winner's row was loaded this step without a wait (bit 5): its
-          // wave writes it into the table now, one more barrier for every wave
-          if ((gl >> 5) & 1u) {
-            if ((tb >> 1) == w) {
-              if ((tb & 1) == 0) {
-                write_row(tb, sg0, sg1, og0);
-                chT0 = pend;
-              } else {
-                write_row(tb, sg0, sg1, og1);
-                chT1 = pend;
-              }
-              pend = -1;
-              ++nwin;
-            }
-            __syncthreads();
-          }
-#endif
           // (the table from the word's VGPR copy: the reads' addresses and the
           // row's u stay in VGPRs, no readfirstlane on the step's chain)
           const uint32_t tbv = (uint32_t)g & 31u;
@@ -4986,14 +4770,6 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
             }
         }
         if (w == 0 && pstar != last) rem[pstar] = (int16_t)mcol;  // (wave 0, every lane)
-#if LB_DEFER
-        if (pend >= 0) {  // a loaded row that did not win: into its table at the next step's top
-          pch = pend;
-          pZ = pslot & 1;
-          pg0 = sg0;
-          pg1 = sg1;
-        }
-#endif
         nrem = last;
         ++t;
         if (!assigned) {
@@ -5005,17 +4781,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
       }
       stamp(4);
       if (big) break;  // (block-uniform: every wave read the same word)
-      // the rows loaded during the Dijkstra into their tables (none is read now)
-      if (pch >= 0) {
-        if (pZ == 0) {
-          write_row(2 * w, pg0, pg1, og0);
-          chT0 = pch;
-        } else {
-          write_row(2 * w + 1, pg0, pg1, og1);
-          chT1 = pch;
-        }
-        pch = -1;
-      }
+      // row cur + 1 into its table (none is read now)
       if (w == NW - 1 && cur + 1 < n) {
         if ((cur + 1) & 1) write_row(2 * NW + 1, cg0, cg1, ogC1);
         else write_row(2 * NW, cg0, cg1, ogC0);
@@ -5055,7 +4821,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         int32_t *o = a.col + (size_t)b * n + 8 * w;
         for (int q = 0; q < 6; ++q) o[q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
         o[6] = (int32_t)nsync;
-        o[7] = (int32_t)(LB_DEFER ? nwin : npre);  // (LB_DEFER: steps this wave won with a row loaded that step)
+        o[7] = 0;  // (was: rows prefetched, a variant not kept)
         // (the synchronous loads' latency, issue to data, in col[b * n + 128 + w])
         a.col[(size_t)b * n + 128 + w] = (int32_t)min(ldlat, (uint64_t)INT32_MAX);
       }
@@ -5304,8 +5070,9 @@ __global__ void unpack_kernel(int16_t *types, const int32_t *rows, int count, co
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < count) {
     const int r = rows[k];
-    if (r >= 0) {
-      for (int m = 0; m <= mode; ++m) types[r + m] = in[k];
+    const int16_t t = in[k];
+    if (r >= 0 && t >= 0) {  // (-1: a padding slot or an out-of-range row's undo entry)
+      for (int m = 0; m <= mode; ++m) types[r + m] = t;
     }
   }
 }
@@ -5834,8 +5601,6 @@ int launch_santa_vt_sc(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
     f.ovf_reset = ctx->d_ovf + (p ^ 1);
     f.undo = nullptr;
     f.nx_rows = nullptr;
-  f.undo = nullptr;
-  f.nx_rows = nullptr;
     rc = launch_santa_vt<0, 0>(ctx, f, B, s);
   }
   if (rc) {
@@ -6110,6 +5875,22 @@ int sh_solve_round(sh_ctx *ctx, int mode, const int32_t *d_rows, int n, int B, i
   if (n <= 0 || n > SH_MAX_N_SANTA) return fail(SH_ERR_ARGS, "n must be in [1, 4096]");
   if ((int64_t)n * (mode + 1) > ctx->nc) return fail(SH_ERR_ARGS, "block larger than the instance");
   if (B < 0) return fail(SH_ERR_ARGS, "B < 0");
+  {  // the next round's rows and the undo record are written while other
+     // workgroups still read this round's rows and types: no overlap allowed
+    auto overlap = [](const void *p, size_t np, const void *q, size_t nq) {
+      const uintptr_t a0 = (uintptr_t)p, b0 = (uintptr_t)q;
+      return p && q && np && nq && a0 < b0 + nq && b0 < a0 + np;
+    };
+    const size_t rows_b = (size_t)n * (size_t)B * 4, types_b = (size_t)ctx->nc * 2;
+    if (sample && (overlap(ext->next_rows, (size_t)n * ext->next_B * 4, d_rows, rows_b) ||
+                   overlap(ext->next_rows, (size_t)n * ext->next_B * 4, d_types, types_b)))
+      return fail(SH_ERR_ARGS, "next_rows overlaps d_rows or d_types");
+    if (ext && ext->d_undo && (overlap(ext->d_undo, (size_t)n * B * 2, d_rows, rows_b) ||
+                               overlap(ext->d_undo, (size_t)n * B * 2, d_types, types_b) ||
+                               (sample && overlap(ext->d_undo, (size_t)n * B * 2, ext->next_rows,
+                                                  (size_t)n * ext->next_B * 4))))
+      return fail(SH_ERR_ARGS, "d_undo overlaps d_rows, d_types or next_rows");
+  }
   HIP_TRY_RC(refuse_retired(flags));
   DeviceGuard dg(ctx->device);
   hipStream_t s = (hipStream_t)stream;

@@ -502,6 +502,38 @@ def assert_disjoint(rows: torch.Tensor, mode: int) -> None:
 _ZEROED = object()  # GPUEngine._zero_ev: the delta was zeroed on the round's stream
 
 
+def _wait_mail(mail, slot: int, seq: int, stream, spin: int = 256, poll: float = 20e-6,
+               check_every: float = 5e-3):
+    """Wait for mailbox slot `slot` to carry sequence number `seq`, then
+    return its (dS_child, dS_gift, None).  A bounded wait, not a spin
+    forever: every `check_every` seconds the publishing stream is queried,
+    which raises a pending asynchronous HIP error (a faulted or aborted block
+    kernel); once the stream is idle, every launch before the publish has run,
+    so a sequence number still missing means the publish never happened (an
+    announce/solve bookkeeping mismatch, a kernel that left early) and the
+    wait raises instead of hanging.  Sequence numbers only grow per context:
+    a larger one in the slot means this round's value was overwritten."""
+    spins = 0
+    next_check = time.perf_counter() + check_every
+    while True:
+        got = mail[4 * slot]
+        if got == seq:
+            return int(mail[4 * slot + 1]), int(mail[4 * slot + 2]), None
+        if got > seq:
+            raise RuntimeError(f"mailbox slot {slot}: sequence {got} overwrote {seq} before it was read")
+        spins += 1
+        if spins <= spin:
+            continue
+        time.sleep(poll)
+        if time.perf_counter() >= next_check:
+            # (query() raises a pending HIP error of the round's kernels; once
+            #  it reports idle, the publish has landed if it ever will)
+            if stream.query() and mail[4 * slot] != seq:
+                raise RuntimeError(f"mailbox slot {slot}: the round's stream is idle but sequence {seq} "
+                                   f"was never published (slot holds {mail[4 * slot]})")
+            next_check = time.perf_counter() + check_every
+
+
 def _wait(stream, ev) -> None:
     """stream waits for ev, unless ev has completed already (then a wait
     would only add a barrier packet between two block kernels)."""
@@ -608,8 +640,13 @@ class GPUEngine:
         them (sh_sample_blocks_undo), or, when the rows were sampled ahead
         (prefetch_blocks: N > 1, behind the previous round's all-gather and
         before its unpack), the types are gathered now (sh_pack_types).  The
-        token's undo(types) scatters them back (sh_unpack_types); it stays
-        valid until round rnd + 2 is sampled (a ring of two buffers)."""
+        token's undo(types) scatters them back (sh_unpack_types).  The rows and
+        undo record live in buffer rnd % RING of a ring of three: round rnd's
+        block kernels sample round rnd + 1's rows into the next buffer
+        (solve_blocks -> sh_solve_round), so the token stays valid until round
+        rnd + 3 is sampled, i.e. until round rnd + 2's kernels run -- after
+        every rollback the loops can ask for (the pipelined loop undoes round
+        rnd while round rnd + 1 is in flight)."""
         ring, main, k = self._ring(mode, n, B, seed, rnd)
         rows, undo, cnt = self._pf_buf[k], self._undo_buf[k], B * n
         if self._pf_ev[k] is not None:
@@ -756,15 +793,11 @@ class GPUEngine:
             self.ctx.publish_delta(d, slot, seq)
         self._zero_ev[d.data_ptr()] = _ZEROED  # (zeroed by the publish, in stream order)
         mail = self.ctx.mailbox
+        stream = torch.cuda.current_stream(d.device)
 
         class _Handle:
             def result(_):
-                spins = 0
-                while mail[4 * slot] != seq:
-                    spins += 1
-                    if spins > 256:
-                        time.sleep(20e-6)
-                return int(mail[4 * slot + 1]), int(mail[4 * slot + 2]), None
+                return _wait_mail(mail, slot, seq, stream)
 
             def restore(_, t):
                 raise RuntimeError("no snapshot was taken for this round (undo protocol)")

@@ -291,3 +291,25 @@ def test_bench_whole_node_cpu_projection():
     # a host with no more threads than leased: the measured figures themselves
     wn = bench.whole_node_cpu(cb, {"nproc": 8, "used": 16})
     assert wn["cores"] == 16 and wn["port_blocks_per_s"] == 100.0
+
+
+def test_bench_whole_node_cpu_capped_at_round_blocks():
+    """Configs with fewer blocks per round than host threads (78 twins blocks,
+    6 blocks of 3000 pairs): a round's blocks are its only parallelism, so the
+    projected whole-host CPU uses at most that many threads, and the measured
+    figure's busy threads are capped the same way (VERDICT r05 weak #6)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    cb = {"value": 160.0, "cores": 16, "round_blocks": 78, "reference_lap_blocks_per_s": 32.0,
+          "b1_blocks_per_s": {"8": 4.0, "16": 8.0}}
+    wn = bench.whole_node_cpu(cb, {"nproc": 256, "used": 16})
+    assert wn["cores"] == 78 and wn["from_cores"] == 16 and wn["round_blocks"] == 78
+    assert wn["port_blocks_per_s"] == 780.0 and wn["reference_lap_blocks_per_s"] == 156.0
+    assert wn["b1_blocks_per_s"] == 39.0
+    # 6 blocks per round on 16 leased threads: 6 busy, no projection beyond them
+    cb = {"value": 12.0, "cores": 16, "round_blocks": 6, "b1_blocks_per_s": {"6": 3.0}}
+    wn = bench.whole_node_cpu(cb, {"nproc": 256, "used": 16})
+    assert wn["cores"] == 6 and wn["from_cores"] == 6 and wn["port_blocks_per_s"] == 12.0
+    assert wn["b1_blocks_per_s"] == 3.0

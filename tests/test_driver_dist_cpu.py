@@ -386,3 +386,40 @@ def test_error_flags_agreed_across_ranks(pipeline, check):
         msg, solved = out[r]
         assert "error flags 0x4" in msg, (r, msg)
         assert solved == (1 if check else 3), (r, solved)
+
+
+def test_mailbox_wait_is_bounded():
+    """GPUEngine's mailbox wait (driver._wait_mail): returns the published
+    sums, raises when the stream went idle without the publish, raises when a
+    later sequence number overwrote the slot, and surfaces a stream error --
+    instead of spinning forever."""
+    from santa_hip.driver import _wait_mail
+
+    class Stream:
+        def __init__(self, idle=True, exc=None):
+            self.idle, self.exc, self.calls = idle, exc, 0
+
+        def query(self):
+            self.calls += 1
+            if self.exc:
+                raise self.exc
+            return self.idle
+
+    mail = [0] * 8
+    mail[4:8] = [7, 11, -3, 0]
+    assert _wait_mail(mail, 1, 7, Stream()) == (11, -3, None)
+    with pytest.raises(RuntimeError, match="never published"):
+        _wait_mail(mail, 0, 5, Stream(idle=True), spin=4, poll=1e-5, check_every=1e-4)
+    with pytest.raises(RuntimeError, match="overwrote"):
+        _wait_mail(mail, 1, 6, Stream())
+    with pytest.raises(ValueError, match="HIP error"):
+        _wait_mail(mail, 0, 5, Stream(idle=False, exc=ValueError("HIP error")), spin=4, poll=1e-5,
+                   check_every=1e-4)
+
+    class Late(Stream):  # the publish lands while the stream is still busy
+        def query(self):
+            self.calls += 1
+            if self.calls == 3:
+                mail[0:3] = [9, 1, 2]
+            return False
+    assert _wait_mail(mail, 0, 9, Late(), spin=4, poll=1e-5, check_every=1e-4) == (1, 2, None)

@@ -290,66 +290,76 @@ def _oracle_round_threaded(mode, wish, t_host, r, ng, threads=16):
 
 @pytest.mark.parametrize("mode,pinned,rounds", [(0, (1, 10, 19), 20), (1, (0, 10), 11)])
 def test_bench_rounds_vs_oracle(sh, ctx, full_data, mode, pinned, rounds):
-    """The rounds bench.py times, pinned to the oracle on the states they
-    actually run from: bench seed 2017, full rounds (3730 singles blocks on the
-    default dispatch: the fused santa_sp3_kernel<.., FUSED = true>, which builds
-    its register tile in-kernel from the packed wishlists and solves in 32-bit
-    lattice keys; 78 twins blocks on santa_block_kernel<1, 1>), the
-    reference's loop (run_rounds) with its default
-    delta round sums.
-      * pinned rounds: ALL blocks' col and exact cost, the whole new type
-        vector, the steps and the deltas equal the oracle solving the same
+    """The rounds bench.py times, pinned to the oracle on the path bench.py
+    runs: bench seed 2017, full rounds (3730 singles blocks on the default
+    dispatch: the fused santa_sp3_kernel<.., FUSED = true>, which samples
+    nothing itself but builds its register tile in-kernel from the packed
+    wishlists and solves in 32-bit lattice keys; 78 twins blocks on
+    santa_block_kernel<1, 1>), the reference's loop (run_rounds) with its
+    default delta round sums.  The engine under test is GPUEngine itself: its
+    solve_blocks runs (ctx.solve_round: the round's undo record written by the
+    block kernels, the next round's rows sampled by them into the ring of
+    three buffers, the delta published to the host mailbox by the round's last
+    launch); the wrapper only reads the state around it.
+      * pinned rounds: ALL blocks' col and exact cost (a separate
+        SH_FLAG_NO_APPLY solve from the saved pre-round state), the steps, and
+        the whole post-round type vector equal the oracle solving the same
         pre-round state;
       * every other round: a random sample of 64 blocks (col, cost, their new
-        types) equals the oracle solving them from the round's pre-round state;
-      * every round: the (S_child, S_gift) the loop reports (start sums + the
-        all-reduced block deltas) equal the oracle's rescore of the round's
+        types) equals the oracle, and the whole post-round vector equals the
+        pre-round one with the NO_APPLY solve's assignment applied;
+      * every round: the rows are the host sampler's (seed, round) blocks, and
+        the (S_child, S_gift) the loop reports (start sums + the block deltas,
+        read through the mailbox) equal the oracle's rescore of the round's
         post-round state (mpi_single.py:151-157, mpi_twins.py:157-169)."""
     from santa_hip import _lib
+    from santa_hip import sampler as S
     from santa_hip.driver import GPUEngine, World, run_rounds
     n = 256
-    _, _, _, nb = ctx.geometry(mode, n)
+    lo, count, stride, nb = ctx.geometry(mode, n)
     assert ctx.solve_design(mode, n, nb) == (_lib.SH_DESIGN_SPARSE3 if mode == 0 else _lib.SH_DESIGN_TWINS)
-    checked, sampled, post = [], [], []
+    checked, sampled, post, fused = [], [], [], []
 
     class Pin(GPUEngine):
         calls = 0
 
-        def solve_blocks(self, mode_, rows_, n_, types_, delta=None):
+        def solve_blocks(self, mode_, rows_, n_, types_, delta=None, steps=None):
             k = self.calls
             self.calls += 1
             B = rows_.numel() // n_
+            fused.append(self._cur is not None and self._cur[6])  # (rows sampled by the last round's kernels)
             pre = types_.cpu().numpy()
             r = rows_.cpu().numpy().reshape(B, n_)
+            assert np.array_equal(r, S.sample_blocks(2017, k, lo, count, stride, n_, B)), k
             col = torch.empty(B * n_, dtype=torch.int32, device="cuda")
             cost = torch.empty(B, dtype=torch.int64, device="cuda")
+            ctx.solve_blocks(mode_, rows_, n_, types_, col=col, cost=cost, flags=_lib.SH_FLAG_NO_APPLY)
+            assert np.array_equal(types_.cpu().numpy(), pre), k
+            st = torch.empty(B, dtype=torch.int64, device="cuda") if k in pinned else steps
+            super().solve_blocks(mode_, rows_, n_, types_, delta=delta, steps=st)
+            got = types_.cpu().numpy()
+            c = col.cpu().numpy().reshape(B, n_)
+            t_host = pre.copy()
             if k not in pinned:
-                self.ctx.solve_blocks(mode_, rows_, n_, types_, col=col, cost=cost, delta=delta)
                 pick = np.sort(np.random.default_rng(1000 + k).choice(B, min(64, B), replace=False))
-                t_host = pre.copy()
                 ocol, ocost, _ = _oracle_round_threaded(mode_, full_data.wish, t_host, r[pick],
                                                         full_data.ng)
-                got = types_.cpu().numpy()
-                assert np.array_equal(col.cpu().numpy().reshape(B, n_)[pick], ocol), k
+                assert np.array_equal(c[pick], ocol), k
                 assert np.array_equal(cost.cpu().numpy()[pick], ocost), k
                 kids = np.concatenate([r[pick].reshape(-1) + m for m in range(mode_ + 1)])
                 assert np.array_equal(got[kids], t_host[kids]), k
+                # the applied round = the pre-round state permuted by the NO_APPLY assignment
+                want = pre.copy()
+                for m in range(mode_ + 1):  # (a unit's members share its first member's type)
+                    want[r + m] = pre[np.take_along_axis(r, c, axis=1)]
+                assert np.array_equal(got, want), k
                 sampled.append(k)
                 return
-            steps = torch.empty(B, dtype=torch.int64, device="cuda")
-            dl = torch.zeros(2, dtype=torch.int64, device="cuda")
-            self.ctx.solve_blocks(mode_, rows_, n_, types_, col=col, cost=cost, delta=dl, steps=steps)
-            if delta is not None:  # (the driver's delta sums: this round's blocks too)
-                delta += dl
-            t_host = pre.copy()
             ocol, ocost, osteps = _oracle_round_threaded(mode_, full_data.wish, t_host, r, full_data.ng)
-            assert np.array_equal(col.cpu().numpy().reshape(B, n_), ocol), k
+            assert np.array_equal(c, ocol), k
             assert np.array_equal(cost.cpu().numpy(), ocost), k
-            assert np.array_equal(types_.cpu().numpy(), t_host), k
-            assert int(steps.sum()) == osteps, k
-            s0 = oracle.score_sums(full_data.wish, full_data.goodkids, pre)
-            s1 = oracle.score_sums(full_data.wish, full_data.goodkids, t_host)
-            assert dl.cpu().tolist() == [s1[0] - s0[0], s1[1] - s0[1]], k
+            assert np.array_equal(got, t_host), k
+            assert int(st.sum()) == osteps, k
             checked.append(k)
 
         def delta_begin(self, t, d, full, after=None, **kw):
@@ -369,6 +379,74 @@ def test_bench_rounds_vs_oracle(sh, ctx, full_data, mode, pinned, rounds):
     assert checked == list(pinned) and res.rounds == rounds
     assert sorted(checked + sampled) == list(range(rounds))
     assert len(post) == rounds and reported == post
+    # every round after the first took its rows from the previous round's block kernels
+    assert fused == [False] + [True] * (rounds - 1)
+    assert ctx.error_flags() == 0
+
+
+def test_twins_rejected_rounds_vs_oracle(sh, ctx, full_data):
+    """Keep-if-improved rounds with rollbacks (mpi_twins.py:133,166-175) on
+    the path the loop runs: 12 full 78-block twins rounds, rounds 1, 4, 5 and
+    9 forced to be rejected (their score is hidden from the loop by a
+    score_from_sums hook, so their update must be undone).
+      * serial loop, GPUEngine (undo records written by the block kernels,
+        rows sampled ahead by them, mailbox sums): every round's pre-state
+        equals the oracle's accepted state -- so every rollback restored it --
+        and every post-round state equals the oracle solving that pre-state;
+      * pipelined loop (speculative round undone and re-run after a
+        rejection) and an engine without undo records (whole-state copies)
+        give the same history and final state."""
+    from santa_hip.driver import GPUEngine, World, run_rounds
+    n, rounds, reject = 256, 12, {1, 4, 5, 9}
+    lo, count, stride, nb = ctx.geometry(1, n)
+    expected = [full_data.types.copy()]
+    pending = []
+
+    def hooked(base):
+        class E(base):
+            calls = 0
+
+            def score_from_sums(self, sc, sg):
+                k = self.calls
+                self.calls += 1
+                s = super().score_from_sums(sc, sg)
+                return float("-inf") if k - 1 in reject else s  # (call 0 is the start score)
+        return E
+
+    class Oracle(hooked(GPUEngine)):
+        def solve_blocks(self, mode_, rows_, n_, types_, delta=None, steps=None):
+            B = rows_.numel() // n_
+            pre = types_.cpu().numpy()
+            assert np.array_equal(pre, expected[-1]), len(pending)
+            super().solve_blocks(mode_, rows_, n_, types_, delta=delta, steps=steps)
+            t_host = pre.copy()
+            _oracle_round_threaded(mode_, full_data.wish, t_host, rows_.cpu().numpy().reshape(B, n_),
+                                   full_data.ng)
+            assert np.array_equal(types_.cpu().numpy(), t_host), len(pending)
+            pending.append(t_host)
+
+    def on_round(st):
+        if st.accepted:
+            expected.append(pending[-1])
+
+    class Copies(hooked(GPUEngine)):
+        sample_round = None
+
+    out = []
+    for eng, pipeline in ((Oracle, False), (hooked(GPUEngine), True), (Copies, False), (Copies, True)):
+        types = ctx.upload_types(full_data.types)
+        res = run_rounds(eng(ctx), types, mode=1, n=n, seed=31, max_rounds=rounds, patience=1 << 30,
+                         world=World(), pipeline=pipeline,
+                         on_round=on_round if eng is Oracle else None)
+        torch.cuda.synchronize()
+        hist = [(st.round, st.s_child, st.s_gift, st.accepted) for st in res.history]
+        out.append((types.cpu().numpy(), hist))
+    kept = [h[3] for h in out[0][1]]
+    assert len(pending) == rounds and len(expected) == 1 + sum(kept)
+    assert not any(kept[r] for r in reject) and sum(kept) >= 4
+    assert np.array_equal(out[0][0], expected[-1])
+    for t, h in out[1:]:
+        assert np.array_equal(t, out[0][0]) and h == out[0][1]
     assert ctx.error_flags() == 0
 
 
