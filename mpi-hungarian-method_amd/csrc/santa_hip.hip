@@ -3105,7 +3105,6 @@ struct Sp3LdsRecord {
   int16_t ctype[256];         // column gift types (old)
   uint8_t own[256];           // code(i, i): row i's own gift
   uint32_t rem[512];          // scipy's `remaining`, then the rows by step (see the solve)
-  uint32_t lol[256 + 4];      // the columns' tie bits (lo) + a dump word (see the solve)
 };
 // Fused design (FUSED = true, round 4): the wave builds its own tile, so no
 // record travels through HBM (santa_tile_kernel wrote ~67 MB per round and
@@ -3124,7 +3123,6 @@ struct Sp3LdsFused {
       int32_t rowc[256 + 32];
       int32_t u_l[256 + 64];
       uint32_t rem[512];
-      uint32_t lol[256 + 4];       // the columns' tie bits (lo) + a dump word
     } s;                           // solve
     struct {
       uint32_t thead[SP4_MAX_NG];  // counting-sort counters, then the type table
@@ -3136,18 +3134,42 @@ struct Sp3LdsFused {
   } u;
 };
 
-// The step's book-keeping (the winner leaves `remaining`, the mover takes its
-// position) changes one column's tie bits: one slot of one lane's four.  The
-// one-wave solvers keep those bits in LDS (lol[j], column j; lol[256] a dump
-// word), write the two changed words with plain DS ops in the next step's LDS
-// group and read the lane's four words back in the same group (in-order LDS:
-// the read sees the writes).  Round 5 updated a register tuple through GPR
-// index mode (s_set_gpr_idx_on) instead; with the tuple pinned to the right
-// registers it still corrupted values of other blocks at random whenever the
-// register allocation changed (VALU results of the other waves of the SIMD
-// written to the wrong register), so no kernel uses GPR indexing
-// or M0-relative moves in inline asm (tests/test_asm_lint_cpu.py).
-constexpr int SP3_LOL_OFF = 512 * 4;  // byte offset of lol from rem (the DS ops' immediate offset)
+// GPR-indexed moves (s_set_gpr_idx_on) in the one-wave solvers: a step's
+// book-keeping writes one slot of a four-register tuple (the winner's tie bits
+// ~0, the mover's xor), a Dijkstra's sink flip and each augmenting hop read or
+// write one slot.  The rules (tests/test_asm_lint_cpu.py checks them):
+//  * the only instruction in index mode is v_mov_b32 (VOP1), the form the
+//    compiler itself emits for dynamic register-array indexing: a read
+//    (gpr_idx(SRC0)) or a write (gpr_idx(DST)) of one slot, a
+//    read-modify-write as read, plain VALU, write, and the lane chosen by an
+//    exec mask.  Round 5's v_cndmask_b32_e64 / v_xor_b32 in index mode were
+//    exact only under round 5's register allocation: every other allocation
+//    (round 6's first builds, a v_cndmask_b32_e32 form too) corrupted
+//    registers of other blocks at random -- whole VGPRs of the output stage,
+//    sometimes a step -- while the v_mov-only form was exact on every run
+//    (tools/diag_round.py, profiles/r06_gpr_idx_diag.jsonl);
+//  * an indexed instruction names the first register of its tuple
+//    literally, and the tuple is an operand of the same asm pinned to those
+//    physical registers ("+{v[B:B+3]}" when written, "{v[B:B+3]}" when only
+//    read), so the compiler knows the whole tuple is read / written;
+//  * every such asm clobbers M0 (s_set_gpr_idx_on writes M0[7:0], [15:12]).
+// The bases are the registers the allocator picks for these tuples anyway.
+#define SH_STR2(x) #x
+#define SH_STR(x) SH_STR2(x)
+#define SH_VREG(b) "v" SH_STR(b)
+#define SH_VTUPLE(b, e) "{v[" SH_STR(b) ":" SH_STR(e) "]}"
+#define SP3_LO_V 78    // santa_sp3_kernel: lo (the step's book-keeping) in v78..v81
+#define SP3_LO_VE 81
+#define SP3_LI_V 66    //                   LI (the sink's tie-bit flip)
+#define SP3_LI_VE 69
+#define SP3_PROW_V 74  //                   prow (the augmentation's path row)
+#define SP3_PROW_VE 77
+#define DT_LO_V 8      // santa_dt_kernel: the same three tuples
+#define DT_LO_VE 11
+#define DT_LI_V 0
+#define DT_LI_VE 3
+#define DT_PROW_V 8
+#define DT_PROW_VE 11
 
 template <bool TIMED, bool FUSED>
 __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const unsigned char *rec_all) {
@@ -3160,12 +3182,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
     rowc = SM.u.s.rowc;
     u_l = SM.u.s.u_l;
     rem = SM.u.s.rem;
-    static_assert(offsetof(Sp3LdsFused, u.s.lol) - offsetof(Sp3LdsFused, u.s.rem) == SP3_LOL_OFF, "lol after rem");
   } else {
     rowc = SM.rowc;
     u_l = SM.u_l;
     rem = SM.rem;
-    static_assert(offsetof(Sp3LdsRecord, lol) - offsetof(Sp3LdsRecord, rem) == SP3_LOL_OFF, "lol after rem");
   }
   auto ovfr = SM.ovfr;
   auto ovf = SM.ovf;
@@ -3452,11 +3472,10 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   //        is the row of step t (rowq, below); ~0: not reached
   //   W    -v_V (the range check, the outputs), Wp = W << SP3_SH (relaxation)
   //   lo   key tie-break bits (class << 10 | pkey << 2 | k); ~0: left
-  //        `remaining` this Dijkstra (or j >= n); held in LDS (lol) and read
-  //        back by every step's LDS group
+  //        `remaining` this Dijkstra (or j >= n)
   uint32_t sbp[4];
   int32_t W[4], Wp[4];
-  u32x4 lo;
+  u32x4 lo;            // (one VGPR tuple: a step's book-keeping writes lo[k] by an indexed move)
   uint32_t c4r = ~0u;  // column of row 4*lane + k in byte k
   uint32_t r4c = 0;    // row of column 4*lane + k in byte k (valid where assigned)
   // the tie bits of column j = 4 lane + k at a Dijkstra's start (pos = n-1-j):
@@ -3464,7 +3483,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
   // with P = pos << 2 | k (255 - pos = pos ^ 255), kept as a table LI that
   // flips by 0x7FC for the one column a Dijkstra assigns (its sink; a column,
   // once assigned, stays so); a column j >= n (never assigned) holds ~0
-  u32x4 LI;
+  u32x4 LI;  // (one VGPR tuple: the sink's flip is an indexed move)
   // `remaining` at a Dijkstra's start: rem[p] = n - 1 - p for this lane's p
   uint4 rem0;
 #pragma unroll
@@ -3475,7 +3494,6 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
     LI[k] = j < n ? (((uint32_t)(n - 1 - j) << 2) | (uint32_t)k) ^ 0x3FCu : ~0u;
   }
   rem0 = make_uint4(n - 1 - 4 * lane, n - 2 - 4 * lane, n - 3 - 4 * lane, n - 4 - 4 * lane);
-  const uint32_t m1 = ~0u;  // (the winner's tie bits: the DS write's data VGPR)
   // rem[p]: the column at position p of scipy's `remaining`; rowq[n - 1 - t]:
   // the LDS address of u_l[i] for the row i of step t (written by the step's
   // LDS group from the address it reads the dual with)
@@ -3509,27 +3527,24 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       // Dijkstra set-up: remaining = [n-1 .. 0], every column < n live, spc = inf
       int ln = lane;
       asm volatile("" : "+v"(ln));
+      lo = LI;
 #pragma unroll
       for (int k = 0; k < 4; ++k) sbp[k] = ~0u;
-      // (rem + 16 lane: this lane's `remaining` words, and at +SP3_LOL_OFF
-      //  its four tie-bit words, lol[4 lane ..] = LI)
-      const uint32_t r16 = lds_addr(rem) + 16u * (uint32_t)ln;
       *(uint4 *)(rem + 4 * ln) = rem0;
-      *(uint4 *)(rem + 4 * ln + SP3_LOL_OFF / 4) = make_uint4(LI[0], LI[1], LI[2], LI[3]);
       int nrem = n;
       uint32_t rq = lds_addr(rem) + 4u * (uint32_t)(n - 1);  // &rem[nrem - 1], stepped down
       asm volatile("" : "+v"(rq));  // (a VGPR: the LDS address operand, stepped by one VALU)
       uint32_t mvb = (uint32_t)SP3_BIAS;  // minVal + BIAS (the key's value field of the last winner)
       int i = cur;
       int sink;
-      // deferred book-keeping of the previous step, applied by the next
-      // step's LDS group: the winner leaves `remaining` (lol[winner] = ~0),
-      // the mover (the column at the last position) takes the winner's
-      // position (lol[mover] ^= kX); both addresses rem + 4 j (+ SP3_LOL_OFF
-      // in the DS op); the first step of a Dijkstra writes the dump word
-      uint32_t wa = lds_addr(rem) + 4u * 256u, ma = wa;
-      uint32_t kX = 0;  // (a VGPR: the xor's data)
-      asm volatile("" : "+v"(kX), "+v"(wa), "+v"(ma));
+      // deferred book-keeping of the previous step, applied in the shadow of
+      // the next step's LDS group: the winner (lane, slot) leaves `remaining`
+      // (lo = ~0), the mover (the column at the last position) takes the
+      // winner's position (its pkey bits ^= kX); a lane mask of 0: none
+      uint64_t wmask = 0, mmask = 0;
+      int kw = 0, kmv = 0;
+      uint32_t kX = 0;  // (a VGPR: the xor's vector operand)
+      asm volatile("" : "+v"(kX));
       bool first = true;
       for (;;) {
         ++steps;
@@ -3562,43 +3577,53 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
         int2 c01, c23;
         // The step's LDS traffic as one issue group for every row (a row with
         // more than 32 hits has the marker, whose slot is a dump slot, in its
-        // entry 31; such a row re-reads its columns below): the previous
-        // step's book-keeping (the winner's tie-bit word written by every
-        // lane, the mover's xor by lane 0: an atomic by 64 lanes would
-        // serialise), the dual and the mover, the scatter, the row reads (two
-        // ds_read_b64 of slots 2l, 2l+1 and 128+2l, 129+2l: one bank per lane
-        // of a 32-lane group, where the ds_read2_b32 pairs were 2-way on both
-        // halves), this lane's four tie-bit words, the un-scatter, the step's
-        // row (rowq[nrem - 1] = the dual's address) -- no wait in between,
-        // one wait at the end.  Operands stay live through that wait.  (The
-        // one-word stores by all 64 lanes -- this rowq entry, rem[pstar] after
-        // the decode -- measured 5 % faster per lone step than the same stores
-        // by one lane under an exec mask: profiles/r04_ab_stores.jsonl.)
+        // entry 31; such a row re-reads its columns below): the dual and the
+        // mover, the scatter, the row reads (two ds_read_b64 of slots 2l, 2l+1
+        // and 128+2l, 129+2l: one bank per lane of a 32-lane group, where the
+        // ds_read2_b32 pairs were 2-way on both halves), the un-scatter, the step's row
+        // (rowq[nrem - 1] = the dual's address) -- no wait in between; then
+        // the previous step's book-keeping in their shadow, one lane and one
+        // slot each: the winner's slot set to ~0 and the mover's slot read,
+        // xor-ed and written back, each lane chosen by exec (the loop runs
+        // with every lane active: exec is restored to -1), each slot by an
+        // indexed v_mov on the lo tuple; one wait at the end.  Operands stay
+        // live through that wait.  (The one-word stores by all 64 lanes --
+        // this rowq entry, rem[pstar] after the decode -- measured 5 % faster
+        // per lone step than the same stores by one lane under an exec mask:
+        // profiles/r04_ab_stores.jsonl.)
         uint32_t ua;  // (u_l + 4 i formed by one VALU: the address is a VGPR operand anyway)
         asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(ua) : "s"(i), "v"(ubv));
         const uint32_t ra = rq;
         const uint32_t sa = lds_addr(rowc) + 4u * (uint32_t)sslot;
         const int32_t miss = SP3_MISS;
-        uint64_t sv;  // (exec, saved around the mover's one-lane xor)
+        uint32_t sv;  // (the mover's slot, read, xor-ed and written back)
         asm volatile(
-            "ds_write_b32 %12, %14 offset:%c17\n\t"
-            "s_mov_b64 %5, exec\n\t"
-            "s_mov_b64 exec, 1\n\t"
-            "ds_xor_b32 %13, %15 offset:%c17\n\t"
-            "s_mov_b64 exec, %5\n\t"
             "ds_read_b32 %0, %6\n\t"
             "ds_read_b32 %1, %7\n\t"
             "ds_write_b32 %8, %9\n\t"
             "ds_read_b64 %2, %10\n\t"
             "ds_read_b64 %3, %10 offset:512\n\t"
-            "ds_read_b128 %4, %16 offset:%c17\n\t"
             "ds_write_b32 %8, %11\n\t"
             "ds_write_b32 %7, %6 offset:1024\n\t"
+            "s_mov_b64 exec, %12\n\t"
+            "s_set_gpr_idx_on %13, gpr_idx(DST)\n\t"
+            "v_mov_b32 " SH_VREG(SP3_LO_V) ", -1\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %14\n\t"
+            "s_set_gpr_idx_on %15, gpr_idx(SRC0)\n\t"
+            "v_mov_b32 %4, " SH_VREG(SP3_LO_V) "\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "v_xor_b32 %4, %16, %4\n\t"
+            "s_set_gpr_idx_on %15, gpr_idx(DST)\n\t"
+            "v_mov_b32 " SH_VREG(SP3_LO_V) ", %4\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, -1\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "=&v"(lo), "=&s"(sv)
-            : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(miss), "v"(wa), "v"(ma), "v"(m1),
-              "v"(kX), "v"(r16), "i"(SP3_LOL_OFF)
-            : "memory");
+            : "=&v"(uraw), "=&v"(mover_v), "=&v"(c01), "=&v"(c23), "=&v"(sv),
+              "+" SH_VTUPLE(SP3_LO_V, SP3_LO_VE)(lo)
+            : "v"(ua), "v"(ra), "v"(sa), "v"(sval), "v"(rob), "v"(miss), "s"(wmask), "s"(kw), "s"(mmask),
+              "s"(kmv), "v"(kX)
+            : "memory", "m0");
         // (a row with more than 32 hits: the tile's entries and the overflow
         // list scattered again, the four columns re-read; the other half's
         // marker only sends a row without overflow through here, count 0)
@@ -3651,17 +3676,17 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
           stamp(tB);
         }
         mvb = g >> SP3_SH;
-        const int kw = (int)(g & 3u);
+        kw = (int)(g & 3u);
         const uint32_t pkey = (g >> 2) & 255u;
         const bool assigned = (g >> 10) & 1u;
         const int lw = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == g));
         const int pstar = assigned ? (int)pkey : 255 - (int)pkey;
         const int last = nrem - 1;
         asm("v_lshlrev_b32 %0, 2, %1" : "=v"(kX) : "s"(last ^ pstar));
+        wmask = 1ull << lw;
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
-        // (the next group's book-keeping addresses: rem + 4 j of the winner and the mover)
-        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(wa) : "s"(4 * lw + kw), "v"(remv));
-        asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(ma) : "s"(mv), "v"(remv));
+        mmask = 1ull << (mv >> 2);
+        kmv = mv & 3;
         {  // rem[pstar] = mover (every lane, same word; a no-op when pstar == last)
           uint32_t pa;
           asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(pa) : "s"(pstar), "v"(remv));
@@ -3682,7 +3707,7 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       // column's path row: the row of the step in sbp's low byte (rowq; an
       // unreached column reads an unused in-bounds word).
       const int32_t minVal = (int32_t)mvb - SP3_BIAS;
-      int32_t prow[4];
+      i32x4 prow;  // (one VGPR tuple: the augmentation selects prow[j & 3] by an indexed move)
       // (the visited columns and the sink only, exec-masked: DESIGN §4.0b; 1 % faster
       //  here, 2-4 % slower in santa_dt_kernel: profiles/r05h_masked_dual_ab.jsonl)
 #pragma unroll
@@ -3699,10 +3724,22 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       }
       if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       {  // the sink is the one column this Dijkstra assigns: flip its start tie bits
-        const int sk = sink & 3;
-        const bool sl = lane == (sink >> 2);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) LI[k] ^= (sl && k == sk) ? 0x7FCu : 0u;
+        uint64_t sv;
+        uint32_t tx;
+        asm volatile(
+            "s_mov_b64 %1, exec\n\t"
+            "s_mov_b64 exec, %3\n\t"
+            "s_set_gpr_idx_on %4, gpr_idx(SRC0)\n\t"
+            "v_mov_b32 %2, " SH_VREG(SP3_LI_V) "\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "v_xor_b32 %2, 0x7fc, %2\n\t"
+            "s_set_gpr_idx_on %4, gpr_idx(DST)\n\t"
+            "v_mov_b32 " SH_VREG(SP3_LI_V) ", %2\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %1"
+            : "+" SH_VTUPLE(SP3_LI_V, SP3_LI_VE)(LI), "=&s"(sv), "=&v"(tx)
+            : "s"(1ull << (sink >> 2)), "s"(sink & 3)
+            : "m0");
       }
       stamp(tD1);
       // augment along the path from the sink back to cur (registers only; at
@@ -3712,8 +3749,14 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
       int j = sink, pi = -1, left = n;
       do {
         const int jl = j >> 2;
-        const int jk = j & 3;  // prow[j & 3] (uniform selects), then lane jl of it
-        const int pv = jk == 0 ? prow[0] : jk == 1 ? prow[1] : jk == 2 ? prow[2] : prow[3];
+        int pv;  // prow[j & 3] (one indexed move), then lane jl of it
+        asm volatile(
+            "s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\t"
+            "v_mov_b32 %0, " SH_VREG(SP3_PROW_V) "\n\t"
+            "s_set_gpr_idx_off"
+            : "=v"(pv)
+            : "s"(j & 3), SH_VTUPLE(SP3_PROW_V, SP3_PROW_VE)(prow)
+            : "m0");
         const int pa = __builtin_amdgcn_readlane(pv, jl);
         pi = (int)(((uint32_t)pa - ubase) >> 2);
         // row pi: its previous column t leaves, j becomes its column
@@ -3840,7 +3883,6 @@ __host__ __device__ __forceinline__ DtLds dt_lds_layout(int n, int ng) {
   L.rows = off;  off += r16((size_t)n * 4);
   L.ctype = off; off += r16((size_t)n * 2);
   L.rem = off;   off += 512 * 4;         // `remaining`, then the rows by step (santa_sp3_kernel)
-  off += (256 + 4) * 4;                  // the columns' tie bits at rem + SP3_LOL_OFF (santa_sp3_kernel)
   L.head = off;  off += r16((size_t)ng * 4);
   L.nxt = off;   off += r16((size_t)n * 2);
   L.total = off;
@@ -3891,14 +3933,14 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
   const uint32_t MK = (uint32_t)SP3_MISS + ((uint32_t)nw1 << 20);
   uint32_t sbp[4];
   int32_t W[4], Wp[4];
-  u32x4 lo;  // (read from LDS by every step's group, as in santa_sp3_kernel)
+  u32x4 lo;
   uint32_t c4r = ~0u, r4c = 0;
   // the tie bits of column j = 4 lane + k at a Dijkstra's start (pos = n-1-j):
   // (assigned ? 256 | pos : 255 - pos) << 2 | k, i.e. P ^ 0x400 or P ^ 0x3FC
   // with P = pos << 2 | k (255 - pos = pos ^ 255), kept as a table LI that
   // flips by 0x7FC for the one column a Dijkstra assigns (its sink; a column,
   // once assigned, stays so); a column j >= n (never assigned) holds ~0
-  u32x4 LI;
+  u32x4 LI;  // (one VGPR tuple: the sink's flip is an indexed move)
   // `remaining` at a Dijkstra's start: rem[p] = n - 1 - p for this lane's p
   uint4 rem0;
 #pragma unroll
@@ -3912,7 +3954,6 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
   uint32_t *rowq = rem + 256;
   const uint32_t ubase = lds_addr(u_l);
   const uint32_t tbase = lds_addr(tile8) + 4u * (uint32_t)lane;
-  const uint32_t m1 = ~0u;  // (the winner's tie bits: the DS write's data VGPR)
   int steps = 0;
   bool bad = (a.flags & (SH_FLAG_TEST_RANGE | SH_FLAG_EXACT_ARGMIN)) != 0 || !LR.ok;
   uint32_t accU = 0, accW = 0;
@@ -3925,18 +3966,18 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       if (cur == n - SP3_PRIO_C) __builtin_amdgcn_s_setprio(0);
       int ln = lane;
       asm volatile("" : "+v"(ln));
+      lo = LI;
 #pragma unroll
       for (int k = 0; k < 4; ++k) sbp[k] = ~0u;
-      const uint32_t r16 = lds_addr(rem) + 16u * (uint32_t)ln;  // (+ SP3_LOL_OFF: this lane's tie bits)
       *(uint4 *)(rem + 4 * ln) = rem0;
-      *(uint4 *)(rem + 4 * ln + SP3_LOL_OFF / 4) = make_uint4(LI[0], LI[1], LI[2], LI[3]);
       if (lane == 0) rowq[n - 1] = ubase + 4u * (uint32_t)cur;  // (step 0's row)
       int nrem = n;
       int32_t minVal = 0;
       int i = cur;
       int sink;
-      uint64_t wmask = 0;  // the previous winner's lane: its one-lane stores (none on step 0)
-      uint32_t kX = 0, wa = 0, ma = 0;  // the previous step's mover xor and the two tie-bit words
+      uint64_t wmask = 0, mmask = 0;
+      int kw = 0, kmv = 0;
+      uint32_t kX = 0;
       uint32_t rpa = 0;   // the previous step's rem[pstar] address
       int mover_v = 0;    // its mover, stored by the group, then replaced by this step's
       for (;;) {
@@ -3947,31 +3988,43 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         const uint32_t ra = lds_addr(rem) + 4u * (uint32_t)(nrem - 1);
         const uint32_t ta = tbase + (uint32_t)i * DT_RS;
         uint64_t sv;
+        uint32_t tx;
         // the step's LDS group (santa_sp3_kernel's, with the tile row read
-        // in place of the scatter / row reads / un-scatter), one wait.  Here
-        // the one-word stores (the previous step's rem[pstar] = mover, this
-        // step's rowq entry, the previous step's two tie-bit words) go by one
-        // lane (exec = the previous winner's lane; none on a Dijkstra's first
-        // step, whose row the set-up stores): 2 % faster per lone step than
-        // by all 64 lanes, the reverse of santa_sp3_kernel
+        // in place of the scatter / row reads / un-scatter), the previous
+        // step's book-keeping in its shadow (santa_sp3_kernel's indexed
+        // v_movs), one wait.  Here the one-word
+        // stores (the previous step's rem[pstar] = mover, this step's rowq
+        // entry) go by one lane (exec = the previous winner's lane; none on a
+        // Dijkstra's first step, whose row the set-up stores): 2 % faster per
+        // lone step than by all 64 lanes, the reverse of santa_sp3_kernel
         // (profiles/r04_ab_dt_stores.jsonl, r04_ab_stores.jsonl)
         asm volatile(
             "s_mov_b64 %3, exec\n\t"
-            "s_mov_b64 exec, %8\n\t"
-            "ds_write_b32 %9, %1\n\t"
-            "ds_write_b32 %6, %5 offset:1024\n\t"
-            "ds_write_b32 %10, %12 offset:%c15\n\t"
-            "ds_xor_b32 %11, %13 offset:%c15\n\t"
+            "s_mov_b64 exec, %9\n\t"
+            "ds_write_b32 %14, %1\n\t"
+            "ds_write_b32 %7, %6 offset:1024\n\t"
             "s_mov_b64 exec, %3\n\t"
-            "ds_read_b32 %2, %7\n\t"
-            "ds_read_b32 %0, %5\n\t"
-            "ds_read_b32 %1, %6\n\t"
-            "ds_read_b128 %4, %14 offset:%c15\n\t"
+            "ds_read_b32 %2, %8\n\t"
+            "ds_read_b32 %0, %6\n\t"
+            "ds_read_b32 %1, %7\n\t"
+            "s_mov_b64 exec, %9\n\t"
+            "s_set_gpr_idx_on %10, gpr_idx(DST)\n\t"
+            "v_mov_b32 " SH_VREG(DT_LO_V) ", -1\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %11\n\t"
+            "s_set_gpr_idx_on %12, gpr_idx(SRC0)\n\t"
+            "v_mov_b32 %5, " SH_VREG(DT_LO_V) "\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "v_xor_b32 %5, %13, %5\n\t"
+            "s_set_gpr_idx_on %12, gpr_idx(DST)\n\t"
+            "v_mov_b32 " SH_VREG(DT_LO_V) ", %5\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %3\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(uraw), "+v"(mover_v), "=&v"(w4), "=&s"(sv), "=&v"(lo)
-            : "v"(ua), "v"(ra), "v"(ta), "s"(wmask), "v"(rpa), "v"(wa), "v"(ma), "v"(m1), "v"(kX),
-              "v"(r16), "i"(SP3_LOL_OFF)
-            : "memory");
+            : "=&v"(uraw), "+v"(mover_v), "=&v"(w4), "=&s"(sv), "+" SH_VTUPLE(DT_LO_V, DT_LO_VE)(lo),
+              "=&v"(tx)
+            : "v"(ua), "v"(ra), "v"(ta), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv), "s"(kX), "v"(rpa)
+            : "memory", "m0");
         const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
         accU |= (uint32_t)ui + LR.CU;
         uint32_t bse = ((uint32_t)(SP3_BIAS - ui) << SP3_SH) - ((uint32_t)nw1 << 20) + (uint32_t)(n - nrem);
@@ -3989,7 +4042,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         const uint32_t rsel = __builtin_amdgcn_ubfe(r4c, best << 3, 8);
         const uint32_t g = wave_min_u32_dpp(best);
         minVal = (int32_t)(g >> SP3_SH) - SP3_BIAS;
-        const int kw = (int)(g & 3u);
+        kw = (int)(g & 3u);
         const uint32_t pkey = (g >> 2) & 255u;
         const bool assigned = (g >> 10) & 1u;
         const int lw = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(best == g));
@@ -3998,9 +4051,9 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         kX = (uint32_t)(last ^ pstar) << 2;
         wmask = 1ull << lw;
         const int mv = __builtin_amdgcn_readfirstlane(mover_v);
+        mmask = 1ull << (mv >> 2);
+        kmv = mv & 3;
         rpa = lds_addr(rem) + 4u * (uint32_t)pstar;  // (stored by the next step's group)
-        wa = lds_addr(rem) + 4u * (uint32_t)(4 * lw + kw);  // (the winner's and the mover's tie bits)
-        ma = lds_addr(rem) + 4u * (uint32_t)mv;
         --nrem;
         sink = 4 * lw + kw;
         i = __builtin_amdgcn_readlane((int)rsel, lw);
@@ -4008,7 +4061,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       }
       // dual update, path rows, augmentation: santa_sp3_kernel's
       const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
-      int32_t prow[4];
+      i32x4 prow;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const bool vk = (lo[k] == ~0u) && (4 * lane + k < n);
@@ -4022,16 +4075,34 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       }
       if (lane == 0) __hip_atomic_fetch_add(u_l + cur, minVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       {  // the sink is the one column this Dijkstra assigns: flip its start tie bits
-        const int sk = sink & 3;
-        const bool sl = lane == (sink >> 2);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) LI[k] ^= (sl && k == sk) ? 0x7FCu : 0u;
+        uint64_t sv;
+        uint32_t tx;
+        asm volatile(
+            "s_mov_b64 %1, exec\n\t"
+            "s_mov_b64 exec, %3\n\t"
+            "s_set_gpr_idx_on %4, gpr_idx(SRC0)\n\t"
+            "v_mov_b32 %2, " SH_VREG(DT_LI_V) "\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "v_xor_b32 %2, 0x7fc, %2\n\t"
+            "s_set_gpr_idx_on %4, gpr_idx(DST)\n\t"
+            "v_mov_b32 " SH_VREG(DT_LI_V) ", %2\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b64 exec, %1"
+            : "+" SH_VTUPLE(DT_LI_V, DT_LI_VE)(LI), "=&s"(sv), "=&v"(tx)
+            : "s"(1ull << (sink >> 2)), "s"(sink & 3)
+            : "m0");
       }
       int j = sink, pi = -1;
       for (int hop = 0; hop <= n; ++hop) {
         const int jl = j >> 2;
-        const int jk = j & 3;
-        const int pv = jk == 0 ? prow[0] : jk == 1 ? prow[1] : jk == 2 ? prow[2] : prow[3];
+        int pv;
+        asm volatile(
+            "s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\t"
+            "v_mov_b32 %0, " SH_VREG(DT_PROW_V) "\n\t"
+            "s_set_gpr_idx_off"
+            : "=v"(pv)
+            : "s"(j & 3), SH_VTUPLE(DT_PROW_V, DT_PROW_VE)(prow)
+            : "m0");
         const int pa = __builtin_amdgcn_readlane(pv, jl);
         pi = (int)(((uint32_t)pa - ubase) >> 2);
         const int pl = pi >> 2, ps = 8 * (pi & 3);
