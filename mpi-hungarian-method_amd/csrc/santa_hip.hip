@@ -406,7 +406,8 @@ struct SolveLds {
   int64_t *u;       // [n]   row duals
   int16_t *c4r;     // [n]   col4row (the result)
   int16_t *r4c;     // [n]   row4col
-  int16_t *path;    // [n]   path dump of the visited columns
+  int16_t *path;    // [n]   path dump of the visited columns (sap_solve_mw: scipy's
+                    //       `remaining` during a Dijkstra's steps, see there)
   uint64_t *red;    // [4 * NW]  step argmin words (3, rotating) + fallback partials [2NW, 4NW);
                     // sap_solve_mw_sc: [SC_RING] words (a ring, re-armed in halves)
 };
@@ -445,6 +446,23 @@ __device__ __forceinline__ uint64_t block_min_u64_rot(uint64_t wmin, uint64_t *s
   }
 }
 
+// Columns of the NW * K * 64 slots, k-major: slot k of wave w, lane l holds
+// column (k * NW + w) * 64 + l, so a column's owner is three shifts away.
+template <int NW, int K>
+__device__ __forceinline__ int mw_col(int w, int k, int lane) {
+  static_assert((NW & (NW - 1)) == 0, "NW a power of two");
+  return (k * NW + w) * WAVE + lane;
+}
+
+// The step's book-keeping (round 6; it was a compare and re-select of the
+// position of each of a thread's K columns every step): scipy's `remaining`
+// lives in LDS (S.path, free during the steps) and its mover rem[last] is
+// read at the step's start; the winner's thread finds it by its tie bits, the
+// mover's by its column (one compare per slot each).  With one slot per
+// thread (K = 1) the positions stay in registers, as before round 6.  The winner's removal
+// mask rm goes to ~0 (a removed column's relaxation r >= minVal >= its spc
+// never updates it; its key's high word is ~0), the mover's position bits
+// flip.  The sink step needs none of it.
 template <int NW, int K, typename Loader, int FB = 10, typename... LA>
 __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, const SolveLds &S, int64_t &steps_out,
                              int &fallbacks, const bool exact, const LA &...la) {
@@ -455,19 +473,28 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
   constexpr uint32_t SAT = SHM << LOB;                // key high words >= SAT: saturated
   constexpr uint32_t LOW = 1u << LOB;                 // key high words < LOW: sb < 2^32
   constexpr int64_t BIAS = 1ll << (63 - LOB);
+  constexpr int WG = NW * WAVE;
+  // REM: `remaining` in LDS (K >= 2); one slot per thread keeps the positions
+  // in registers (A/B round 6: the LDS form cost n = 256 blocks ~8 %)
+  constexpr bool REM = K >= 2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int col0 = mw_col<NW, K>(w, 0, lane);  // (slot k holds column col0 + k * NW * 64)
   const int64_t INF = INT64_MAX;
   int64_t spc[K], nv[K];  // nv = -v (column duals, negated)
-  int path[K], pos[K], r4c[K];
-  uint32_t lo[K];  // tie-break bits of the column (cached; the mover's flip per step)
+  int path[K], r4c[K];
+  uint32_t lo[K];  // tie-break bits of the column (the mover's flip per step)
+  uint32_t rm[K];  // ~0: the column left `remaining` this Dijkstra (or j >= n)
+  int pos[K];      // (!REM) the column's position in `remaining`
+  int16_t *rem = S.path;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     nv[k] = 0;
     path[k] = -1;
   }
   auto lo_of = [&](int k, int j) -> uint32_t {
-    return (r4c[k] < 0) ? (((FM - (uint32_t)pos[k]) << FB) | (uint32_t)j)
-                        : ((1u << (2 * FB)) | ((uint32_t)pos[k] << FB) | (uint32_t)r4c[k]);
+    const uint32_t pos = (uint32_t)(n - 1 - j);
+    return (r4c[k] < 0) ? (((FM - pos) << FB) | (uint32_t)j)
+                        : ((1u << (2 * FB)) | (pos << FB) | (uint32_t)r4c[k]);
   };
   int64_t steps = 0;
   int par = 0;  // rotating step-argmin word (0..2)
@@ -476,18 +503,29 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
   for (int cur = 0; cur < n; ++cur) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int j = w * (WAVE * K) + k * WAVE + lane;
+      const int j = mw_col<NW, K>(w, k, lane);
       spc[k] = INF;
-      pos[k] = (j < n) ? (n - 1 - j) : -1;
       r4c[k] = (j < n) ? S.r4c[j] : -1;
       lo[k] = lo_of(k, j);
+      rm[k] = (j < n) ? 0u : ~0u;
+      pos[k] = n - 1 - j;
+    }
+    if constexpr (REM) {
+      for (int p = tid; p < n; p += WG) rem[p] = (int16_t)(n - 1 - p);
+      __syncthreads();
     }
     int nrem = n;
+    int jm_prev = 0, ps_prev = -1;  // the previous step's write rem[ps_prev] = jm_prev
     int64_t minVal = 0;
     int i = cur;
     int sink;
     for (;;) {
       ++steps;
+      const int last = nrem - 1;
+      // the mover's column, read now (its latency hides under the step): every
+      // write to rem is ordered before this read by a barrier except the
+      // previous step's (tid 0's, after that step's fold), patched in below
+      const int jm_raw = REM ? rem[last] : 0;
       const int64_t ui = S.u[i];
       int64_t c[K];
       ld.load(i, c, la...);
@@ -497,9 +535,8 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
       uint64_t best = ~0ull;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const bool act = pos[k] >= 0;
         const int64_t r = c[k] + kU + nv[k];
-        const bool upd = act && (r < spc[k]);
+        const bool upd = r < spc[k];  // (never for a removed column, see above)
         spc[k] = upd ? r : spc[k];
         path[k] = upd ? i : path[k];
         // key = (sb << LOB) | lo with sb = spc - minVal + BIAS.  The high word
@@ -508,12 +545,18 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
         // step of a Dijkstra can relax below minVal = 0 when C < v) gives
         // high words < 2^LOB, below every other key; a winner in either band
         // is re-decided by the exact argmin below
-        const uint64_t sb = (uint64_t)spc[k] + kb;
+        // (one v_lshl_add_u64: written as spc + kb the compiler re-associates
+        //  it to spc - minVal, a carry pair, then adds BIAS's high word)
+        uint64_t sb;
+        if constexpr (K >= 2)  // (A/B round 6: neutral at K = 1)
+          asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(sb) : "v"(spc[k]), "v"(kb));
+        else
+          sb = (uint64_t)spc[k] + kb;
         const uint32_t sh = (uint32_t)(sb >> 32), sl = (uint32_t)sb;
         const uint32_t shc = (uint32_t)min(max((int)sh, 0), (int)SHM);
-        const uint32_t kh = __builtin_amdgcn_alignbit(shc, sl, 32 - LOB);
+        const uint32_t kh = __builtin_amdgcn_alignbit(shc, sl, 32 - LOB) | rm[k];
         const uint64_t key = ((uint64_t)kh << 32) | ((sl << LOB) | lo[k]);
-        best = (act && key < best) ? key : best;
+        best = key < best ? key : best;
       }
       uint64_t g;
       if constexpr (NW == 1) {
@@ -538,13 +581,13 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
         uint64_t m = ~0ull;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-          if (pos[k] >= 0) m = umin64(m, (uint64_t)spc[k] ^ SIGN64);
+          if (!rm[k]) m = umin64(m, (uint64_t)spc[k] ^ SIGN64);
         m = block_min_u64<NW>(wave_min_u64_dpp(m), S.red + 2 * NW, w);
         const int64_t ms = (int64_t)(m ^ SIGN64);
         uint64_t b2 = ~0ull;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          if (pos[k] >= 0 && spc[k] == ms) b2 = umin64(b2, lo[k]);
+          if (!rm[k] && spc[k] == ms) b2 = umin64(b2, lo[k]);
         }
         g = block_min_u64<NW>(wave_min_u64_dpp(b2), S.red + 3 * NW, w);
         minVal = ms;
@@ -560,28 +603,47 @@ __device__ __forceinline__ void sap_solve_mw(const int n, const Loader &ld, cons
       const int pk = (int)((glo >> FB) & FM);
       const int aux = (int)(glo & FM);
       const int pstar = assigned ? pk : (int)FM - pk;
-      const int last = nrem - 1;
-      const uint32_t kX = (uint32_t)(last ^ pstar) << FB;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int p = pos[k];
-        lo[k] ^= (p == last) ? kX : 0u;  // the mover's position key
-        pos[k] = (p == pstar) ? -1 : ((p == last) ? pstar : p);
-      }
       --nrem;
       if (!assigned) {
         sink = aux;
         break;
+      }
+      {  // book-keeping: the winner leaves `remaining` -- its thread knows it by
+         // its tie bits, unique per column -- and the mover (rem[last]) takes
+         // position pstar (branch-free: a scalar branch on the owner put a
+         // chain of SALU on the step's latency path)
+        const uint32_t kX = (uint32_t)(last ^ pstar) << FB;
+        if constexpr (REM) {
+          const uint32_t wl = glo & ((1u << LOB) - 1u);
+#pragma unroll
+          for (int k = 0; k < K; ++k) rm[k] = (lo[k] == wl) ? ~0u : rm[k];
+          const uint32_t jm = (uint16_t)(last == ps_prev ? jm_prev : __builtin_amdgcn_readfirstlane(jm_raw));
+          if (tid == 0) rem[pstar] = (int16_t)jm;  // (a no-op when pstar == last)
+          jm_prev = (int)jm;
+          ps_prev = pstar;
+#pragma unroll
+          for (int k = 0; k < K; ++k) lo[k] ^= ((int)jm - k * NW * WAVE == col0) ? kX : 0u;
+        } else {
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const int p = pos[k];
+            lo[k] ^= (p == last) ? kX : 0u;
+            rm[k] = (p == pstar) ? ~0u : rm[k];
+            pos[k] = (p == last) ? pstar : p;
+          }
+        }
       }
       i = aux;
     }
     // Dual update (scipy: u[cur] += minVal; u[i] += minVal - spc[col4row[i]]
     // for the other visited rows; v[j] -= minVal - spc[j] for visited cols)
     // and path dump of the visited columns.
+    // (S.path is free again: every read of `remaining` preceded the sink
+    // step's fold barrier -- or, NW == 1, is earlier in program order)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int j = w * (WAVE * K) + k * WAVE + lane;
-      if (j < n && pos[k] < 0) {
+      const int j = mw_col<NW, K>(w, k, lane);
+      if (j < n && (rm[k] || j == sink)) {  // (the visited columns; the sink's d is 0)
         const int64_t d = minVal - spc[k];
         nv[k] = nv[k] + d;
         if (r4c[k] >= 0) S.u[r4c[k]] = S.u[r4c[k]] + d;
@@ -1055,9 +1117,9 @@ struct TileU8Loader {  // singles: uint8 rank codes, row stride RS bytes (costs 
   int64_t E;
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint8_t *p = tile + (size_t)i * RS + w * (WAVE * K) + lane;
+    const uint8_t *p = tile + (size_t)i * RS + mw_col<NW, K>(w, 0, lane);
 #pragma unroll
-    for (int k = 0; k < K; ++k) c[k] = (int64_t)((uint64_t)single_cost(p[k * WAVE], nw1, E) << SH);
+    for (int k = 0; k < K; ++k) c[k] = (int64_t)((uint64_t)single_cost(p[k * NW * WAVE], nw1, E) << SH);
   }
 };
 
@@ -1123,20 +1185,17 @@ struct TileU16Loader {  // twins: uint16 entries (twin_entry), row stride RS ele
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // (i < 256, RS < 2^24: a 24-bit multiply, full rate, where i comes from a VGPR)
-    const uint16_t *p = tile + __umul24((uint32_t)i, (uint32_t)RS) + w * (WAVE * K) + lane;
+    const uint16_t *p = tile + __umul24((uint32_t)i, (uint32_t)RS) + mw_col<NW, K>(w, 0, lane);
 #pragma unroll
     for (int k = 0; k < K; ++k)  // (lanes past n read any entry: any value, never used)
-      c[k] = twin_entry_cost<SH>(p[k * WAVE], E32);
+      c[k] = twin_entry_cost<SH>(p[k * NW * WAVE], E32);
   }
 };
 
 // The large-block kernel's twins rows (santa_big_kernel, n > 256) still look
-// their cost up in an LDS table of every (cls, a): index cls << 8 | a.
-__device__ __forceinline__ uint32_t twin_lut_index(uint32_t code16, int nw1) {
-  const uint32_t c1 = code16 & 0xFFu, c2 = code16 >> 8;
-  const uint32_t a = (c1 ? nw1 - c1 : 0u) + (c2 ? nw1 - c2 : 0u);
-  return ((uint32_t)(c1 != 0) + (uint32_t)(c2 != 0)) << 8 | a;
-}
+// their cost up in an LDS table of every (cls, a): index cls << 8 | a, cls =
+// the number of members that wish the column's type, a = the sum of their
+// wish values (WishRowLoader::put builds it).
 __device__ __forceinline__ int64_t twin_lut_cost(uint32_t idx, int64_t E) {
   const int cls = (int)(idx >> 8), a = (int)(idx & 0xFFu);
   const int64_t m = cls == 2 ? 0 : (cls == 1 ? one_hit_residual(a, E) : 2 * E);
@@ -1152,7 +1211,7 @@ struct GlobalLoader {  // generic LSAP: rows streamed from global memory
     const S *row = base + (size_t)i * n;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int j = w * (WAVE * K) + k * WAVE + lane;
+      const int j = mw_col<NW, K>(w, k, lane);
       c[k] = (j < n) ? (int64_t)row[j] : 0;
     }
   }
@@ -1168,7 +1227,7 @@ struct HashLoader {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int j = w * (WAVE * K) + k * WAVE + lane;
+      const int j = mw_col<NW, K>(w, k, lane);
       c[k] = (j < n) ? (int64_t)(sh_hash_cost(seed, b, (uint64_t)i, (uint64_t)j) % (uint64_t)mod) : 0;
     }
   }
@@ -4180,26 +4239,41 @@ struct WishRowLoader {
   const int32_t *rows;    // LDS [n]
   const uint32_t *thead;  // LDS [ng]: end in csort | count << 16
   const uint16_t *csort;  // LDS [n]
-  uint8_t *rowbuf;        // LDS [n] (singles) / [2n] (twins: c1 | c2 << 8) / [4n] (triplets)
+  uint8_t *rowbuf;        // LDS [n] (singles) / [4n] (twins: the twin_lut index, see put) / [4n] (triplets)
   int n, nw, nw1;
   int64_t E;
-  const int64_t *lut;     // twins: twin_lut_index -> exact cost (LDS), as the 4-wave twins kernel
+  const int64_t *lut;     // twins: cls << 8 | a -> exact cost (LDS)
   static constexpr int M = MODE + 1;                     // children per unit
-  static constexpr int BPC = MODE == 0 ? 1 : 2 * MODE;  // rowbuf bytes per column
+  static constexpr int BPC = MODE == 0 ? 1 : 4;  // rowbuf bytes per column
   static_assert(NW * WAVE >= (MODE + 1) * 127, "one thread per wish of a unit (n_wish <= 127)");
   // the code of wish rank r of member vr to every column of gift type g
   __device__ __forceinline__ void put(int g, int vr, int r) const {
     const uint32_t h = thead[g];
     const int cnt = (int)(h >> 16), e = (int)(h & 0xFFFFu);
-    const uint8_t code = (uint8_t)(r + 1);
     // the type's first three columns read before any write (csort is padded:
     // reads past the type are unused), the rest in a loop
     const int b = e - cnt;
     const int x0 = csort[b], x1 = csort[b + 1], x2 = csort[b + 2];
-    if (cnt > 0) rowbuf[BPC * x0 + vr] = code;
-    if (cnt > 1) rowbuf[BPC * x1 + vr] = code;
-    if (cnt > 2) rowbuf[BPC * x2 + vr] = code;
-    for (int x = b + 3; x < e; ++x) rowbuf[BPC * csort[x] + vr] = code;
+    if constexpr (MODE == 1) {
+      // twins: each member ADDS 1 << 8 | its wish value (n_wish - r) to the
+      // column's word, which so becomes the lut index cls << 8 | a itself:
+      // the read decodes nothing (round 6: 11 VALU per column per step).
+      // (cls <= 2, a <= 254: the wishlists are distinct, checked at
+      // sh_ctx_create; the lut at LDS offset 0 with byte-offset words saved
+      // one more VALU at 3000 pairs but cost n <= 1024 2-3 %: not kept)
+      uint32_t *rb = (uint32_t *)rowbuf;
+      const uint32_t add = (1u << 8) | (uint32_t)(nw - r);
+      if (cnt > 0) atomicAdd(rb + x0, add);
+      if (cnt > 1) atomicAdd(rb + x1, add);
+      if (cnt > 2) atomicAdd(rb + x2, add);
+      for (int x = b + 3; x < e; ++x) atomicAdd(rb + csort[x], add);
+    } else {
+      const uint8_t code = (uint8_t)(r + 1);
+      if (cnt > 0) rowbuf[BPC * x0 + vr] = code;
+      if (cnt > 1) rowbuf[BPC * x1 + vr] = code;
+      if (cnt > 2) rowbuf[BPC * x2 + vr] = code;
+      for (int x = b + 3; x < e; ++x) rowbuf[BPC * csort[x] + vr] = code;
+    }
   }
   __device__ __forceinline__ void load(int i, int64_t (&c)[K]) const {
     const int tid = threadIdx.x;
@@ -4222,14 +4296,14 @@ struct WishRowLoader {
     //  columns, so no per-column branch; columns >= n are inactive)
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int j = w * (WAVE * K) + k * WAVE + lane;
+      const int j = mw_col<NW, K>(w, k, lane);
       if (MODE == 2) {
         uint32_t *rb = (uint32_t *)rowbuf;
         c[k] = triplet_cost(rb[j], nw1, E);
         rb[j] = 0;
       } else if (MODE == 1) {
-        uint16_t *rb = (uint16_t *)rowbuf;
-        c[k] = lut[twin_lut_index(rb[j], nw1)];  // (one LDS read instead of the float32 rounding)
+        uint32_t *rb = (uint32_t *)rowbuf;
+        c[k] = lut[rb[j] & (TWIN_LUT - 1)];  // (the mask: a provable bound, the word is < 3 << 8)
         rb[j] = 0;
       } else {
         c[k] = single_cost(rowbuf[j], nw1, E);
@@ -4257,7 +4331,7 @@ __host__ __device__ __forceinline__ BigLds big_lds_layout(int n, int mode, int n
   L.ctype = o;  o += r16((size_t)n * 2);
   L.csort = o;  o += r16((size_t)(n + 2) * 2);  // (+2: the row rebuild reads three entries per type)
   L.thead = o;  o += r16((size_t)ng * 4);
-  L.rowbuf = o; o += r16((size_t)(nw * 64 * k) * (mode == 0 ? 1 : 2 * mode));
+  L.rowbuf = o; o += r16((size_t)(nw * 64 * k) * (mode == 0 ? 1 : 4));
   L.part = o;   o += r16((size_t)nw * 3 * 8);
   L.scan = o;   o += r16((size_t)nw * 4);
   L.lut = o;    o += mode == 1 ? (size_t)TWIN_LUT * 8 : 0;
