@@ -1350,7 +1350,8 @@ __host__ __device__ __forceinline__ SantaLds santa_lds_layout(int n, int mode, i
 // tables), the type -> column chains, then the rank code of every wish into
 // tile8[i * RS + j] (twins: code pairs).  All SANTA_WG threads call it; false
 // (after setting the error flag) when the block's rows or types are bad.
-template <int MODE>
+// (FILL: the tile's miss byte; santa_dt_kernel uses 0xFF, see there)
+template <int MODE, uint8_t FILL = 0>
 __device__ __forceinline__ bool lds_tile_build(const SantaArgs &a, const int b, const int n, const int RS,
                                                uint8_t *tile8, int32_t *rows_l, int16_t *ctype, int32_t *head,
                                                int16_t *nxt) {
@@ -1370,7 +1371,8 @@ __device__ __forceinline__ bool lds_tile_build(const SantaArgs &a, const int b, 
   {
     uint4 *t4 = (uint4 *)tile8;
     const int n16 = (int)((size_t)n * RS * (MODE ? 2 : 1) / 16);
-    for (int q = tid; q < n16; q += SANTA_WG) t4[q] = make_uint4(0, 0, 0, 0);
+    const uint32_t f = 0x01010101u * FILL;
+    for (int q = tid; q < n16; q += SANTA_WG) t4[q] = make_uint4(f, f, f, f);
   }
   // -- column gift types (range-checked: they index LDS tables) -----------
   int badt = 0;
@@ -1465,7 +1467,7 @@ __device__ __forceinline__ bool lds_tile_build(const SantaArgs &a, const int b, 
 // lds_tile_build instead).  All SANTA_WG threads call it; n <= SANTA_WG;
 // gift ids < FAST_MAX_NG (10-bit packed rows).
 constexpr int FAST_MAX_NG = 1024;
-template <int MODE>
+template <int MODE, uint8_t FILL = 0>
 __device__ __forceinline__ bool fast_tile_build(const SantaArgs &a, const int b, const int n, const int RS,
                                                 uint8_t *tile8, int32_t *rows_l, int16_t *ctype, uint32_t *thead,
                                                 uint8_t *csort, uint32_t *wsum, uint8_t *dump, bool &decline) {
@@ -1493,7 +1495,8 @@ __device__ __forceinline__ bool fast_tile_build(const SantaArgs &a, const int b,
   {  // zero the tile
     uint4 *t4 = (uint4 *)tile8;
     const int n16 = (int)((size_t)n * RS * (MODE + 1) / 16);
-    for (int q = tid; q < n16; q += SANTA_WG) t4[q] = make_uint4(0, 0, 0, 0);
+    const uint32_t f = 0x01010101u * FILL;
+    for (int q = tid; q < n16; q += SANTA_WG) t4[q] = make_uint4(f, f, f, f);
   }
   if (__syncthreads_or(live && (ty < 0 || ty >= a.ng))) {
     if (tid == 0) atomicOr(a.err, SH_ERRF_TYPE);
@@ -3931,6 +3934,11 @@ __global__ __launch_bounds__(WAVE, 4) void santa_sp3_kernel(SantaArgs a, const u
 // santa_sp3_kernel.  LDS: the 64 KB tile + ~10 KB, two blocks per CU.
 // ---------------------------------------------------------------------------
 constexpr int DT_RS = 256;  // tile row stride (bytes): a lane's four columns are one dword
+// the tile's miss byte: with 255 for a miss, a column's key-unit cost is
+// min(code << 20, MK) -- a wish's code << 20 is below MK and 255 << 20
+// above it (n_wish <= 253) -- two VALU instead of a shift, a compare and a
+// select (round 6)
+constexpr uint8_t DT_MISS = 0xFF;
 struct DtLds {
   size_t tile, u, rows, ctype, rem, head, nxt, total;
 };
@@ -3966,12 +3974,12 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
     // else / when it declines the type -> column chains
     bool decline = a.wish10 == nullptr || a.ng > FAST_MAX_NG;
     if (!decline &&
-        !fast_tile_build<0>(a, b, n, DT_RS, tile8, rows_l, ctype, (uint32_t *)(smem + L.head), smem + L.nxt,
+        !fast_tile_build<0, DT_MISS>(a, b, n, DT_RS, tile8, rows_l, ctype, (uint32_t *)(smem + L.head), smem + L.nxt,
                             (uint32_t *)(smem + L.u), tile8 + (size_t)n * DT_RS + tid, decline) &&
         !decline)
       return;
     if (decline &&
-        !lds_tile_build<0>(a, b, n, DT_RS, tile8, rows_l, ctype, (int32_t *)(smem + L.head),
+        !lds_tile_build<0, DT_MISS>(a, b, n, DT_RS, tile8, rows_l, ctype, (int32_t *)(smem + L.head),
                            (int16_t *)(smem + L.nxt)))
       return;
   }
@@ -3990,6 +3998,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
   // folded into the step's scalar: a wish (c - nw1) * 512 and a miss 1 in
   // V units, i.e. a miss enters as MK = 2^11 + (nw1 << 20)
   const uint32_t MK = (uint32_t)SP3_MISS + ((uint32_t)nw1 << 20);
+  uint32_t v20 = 20;  // (the SDWA shifts' amount, in a VGPR)
+  asm volatile("" : "+v"(v20));
   uint32_t sbp[4];
   int32_t W[4], Wp[4];
   u32x4 lo;
@@ -4091,8 +4101,21 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         uint32_t best = ~0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const uint32_t code = (w4 >> (8 * k)) & 0xFFu;
-          const uint32_t c = code ? code << 20 : MK;
+          // byte k << 20 in one SDWA shift (the compiler's shift + and is two)
+          uint32_t cs;
+          if (k == 0)
+            asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+                : "=v"(cs) : "v"(v20), "v"(w4));
+          else if (k == 1)
+            asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+                : "=v"(cs) : "v"(v20), "v"(w4));
+          else if (k == 2)
+            asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+                : "=v"(cs) : "v"(v20), "v"(w4));
+          else
+            asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+                : "=v"(cs) : "v"(v20), "v"(w4));
+          const uint32_t c = min(cs, MK);  // (DT_MISS)
           const uint32_t r = (uint32_t)Wp[k] + c + bse;
           sbp[k] = r < sbp[k] ? r : sbp[k];
           const uint32_t key = (sbp[k] & SP3_KMASK) | lo[k];
@@ -4194,8 +4217,8 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
     const int i = 4 * lane + k;
     if (i < n) {
       const int col = (int)((c4r >> (8 * k)) & 0xFFu);
-      const uint32_t cn = tile8[(size_t)i * DT_RS + col];
-      const uint32_t co = tile8[(size_t)i * DT_RS + i];
+      const uint32_t tn = tile8[(size_t)i * DT_RS + col], to = tile8[(size_t)i * DT_RS + i];
+      const uint32_t cn = tn == DT_MISS ? 0u : tn, co = to == DT_MISS ? 0u : to;
       const int told = ctype[i], tnew = ctype[col];
       const int chd = rows_l[i];
       cost += single_cost(cn, nw1, E);
@@ -5760,10 +5783,11 @@ int launch_santa_vt_sc(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
 // left (out of range; every block under the exact-argmin and range test
 // flags).  Counters alternate as in launch_santa_sp.
 int launch_santa_dt(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
-  // the tile holds rank codes (rank + 1) in uint8 with 255 reserved: the same
-  // guard as the default dispatch, here also for the forced SH_FLAG_DT_TILE
-  // (sh_ctx_create caps n_wish at 127 today, well inside it)
-  if (ctx->n_wish > 254) return fail(SH_ERR_ARGS, "dense tile: n_wish > 254 does not fit the uint8 rank codes");
+  // the tile holds rank codes (rank + 1) in uint8 with 255 the miss, and a
+  // miss's key-unit cost (n_wish + 1) << 20 | 2^11 must stay below 255 << 20:
+  // the same guard as the default dispatch, here also for the forced
+  // SH_FLAG_DT_TILE (sh_ctx_create caps n_wish at 127 today, well inside it)
+  if (ctx->n_wish > 253) return fail(SH_ERR_ARGS, "dense tile: n_wish > 253 does not fit the uint8 rank codes");
   const size_t lds = dt_lds_layout(a.n, ctx->ng).total;
   if (lds > 160 * 1024) return fail(SH_ERR_ARGS, "dense tile: too many gift types for LDS");
   static thread_local AttrCache attr;
@@ -5948,7 +5972,7 @@ int pick_design(sh_ctx *ctx, int mode, int n, int B, unsigned flags) {
   // / 0.65 ms at round 10; profiles/r04_shard_dt.jsonl).  Beyond it the
   // sparse kernel: at 933 blocks (the shard at 4 GPUs) 1.52 ms against 1.60
   // for the 4-wave register tile and 1.76 for two waves of dense-tile blocks.
-  if (ctx->n_wish <= 254 && B <= dt_tile_slots(ctx, n)) return SH_DESIGN_DT_TILE;
+  if (ctx->n_wish <= 253 && B <= dt_tile_slots(ctx, n)) return SH_DESIGN_DT_TILE;
   return sparse;
 }
 
