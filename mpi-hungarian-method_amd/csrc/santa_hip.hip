@@ -4692,6 +4692,54 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
     if (tid == 0) atomicOr(a.err, SH_ERRF_TYPE);
     return;
   }
+  // -- slots: the columns sorted by gift type (round 6) -------------------------------
+  // A step reads each column's cost as tbl[table][type]: with the columns in
+  // their block order a wave's 64 int16 reads hit random banks (48 % of the
+  // LDS-active cycles were bank conflicts); with slot s = (w K + k) 64 + lane
+  // holding the columns in type order they hit a few consecutive words.  Every
+  // index of the solve (keys' column field, rem, c4r / r4c, path) is a slot;
+  // only the tie bits use the column's own position n - 1 - pk (scipy's
+  // `remaining` order), so the decisions -- every key is unique by its tie
+  // bits -- do not depend on the layout.  c4r goes back to columns at the end.
+  // The padding (columns >= n) sorts last: slot < n <=> a real column.
+  int pk[K];  // the column of each of this thread's slots
+  {
+    uint32_t *cnt = (uint32_t *)(smem + L.tbl);  // [ng + 1] (scratch: the tables are set below)
+    int16_t *pslot = (int16_t *)(smem + L.u);    // [NCOL] slot -> column (scratch: u is set below)
+    uint32_t *wsum = (uint32_t *)(smem + L.part);
+    const int nt = a.ng + 1;
+    for (int t = tid; t < nt; t += WG) cnt[t] = 0u;
+    __syncthreads();
+    for (int j = tid; j < NCOL; j += WG) atomicAdd(&cnt[j < n ? (int)ctype[j] : a.ng], 1u);
+    __syncthreads();
+    const int per = (nt + WG - 1) / WG, t0 = min(nt, tid * per), t1 = min(nt, t0 + per);
+    uint32_t sum = 0;
+    for (int t = t0; t < t1; ++t) sum += cnt[t];
+    const uint32_t incl = wave_incl_scan_u32(sum);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (int q = 0; q < w; ++q) run += wsum[q];
+    for (int t = t0; t < t1; ++t) {
+      const uint32_t c = cnt[t];
+      cnt[t] = run;
+      run += c;
+    }
+    __syncthreads();
+    for (int j = tid; j < NCOL; j += WG) pslot[atomicAdd(&cnt[j < n ? (int)ctype[j] : a.ng], 1u)] = (int16_t)j;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) pk[k] = pslot[(w * K + k) * WAVE + lane];
+    __syncthreads();  // (the scratch areas are set below)
+  }
+  // `remaining` at a Dijkstra's start: rem[p] = the slot of column n - 1 - p
+  auto rem_init = [&]() {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int sl = (w * K + k) * WAVE + lane;
+      if (sl < n) rem[n - 1 - pk[k]] = (int16_t)sl;
+    }
+  };
   {  // every table entry a miss (V = 1), every u entry 0
     uint32_t *t32 = (uint32_t *)tbl;
     const int nd = (2 * NW + 2) * TS / 2;
@@ -4701,8 +4749,8 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
     u32[i] = 0;
     c4r[i] = -1;
     r4c_l[i] = -1;
-    rem[i] = (int16_t)(n - 1 - i);
   }
+  rem_init();
   if (tid < 3) words[tid] = ~0ull;
   __syncthreads();
 
@@ -4720,7 +4768,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
     int32_t ucol[K];         // u of row4col
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      ct[k] = ctype[(w * K + k) * WAVE + lane];
+      ct[k] = ctype[pk[k]];  // (padding: type 0, never read as a live column)
       W[k] = 0;
     }
     // this wave's tables 2w, 2w + 1: the children they hold and, per lane, the
@@ -4774,11 +4822,11 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
     for (int cur = 0; cur < n; ++cur) {
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const int j = (w * K + k) * WAVE + lane;
+        const int j = (w * K + k) * WAVE + lane;  // (the slot)
         const int rr = j < n ? r4c_l[j] : -1;
         info[k] = rr >= 0 ? ((uint32_t)rows_l[rr] << 11) | (uint32_t)rr : ~0u;
         ucol[k] = rr >= 0 ? u32[rr] : 0;
-        const int p = n - 1 - j;
+        const int p = n - 1 - pk[k];  // (the column's position: scipy's order)
         lo[k] = j >= n ? ~0u : rr < 0 ? (uint32_t)(2047 - p) : (2048u | (uint32_t)p);
         sbp[k] = ~0u;
       }
@@ -4980,7 +5028,7 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
         }
         big |= pi != cur;
       }
-      for (int p = tid; p < n; p += WG) rem[p] = (int16_t)(n - 1 - p);
+      rem_init();
       __syncthreads();
     }
     stamp(5);
@@ -5001,6 +5049,16 @@ __global__ __launch_bounds__(NW * WAVE) void santa_lb_kernel(SantaArgs a) {
   if (__syncthreads_or(big)) {  // left untouched: solved by the fallback launch
     if (tid == 0) a.ovf_list[atomicAdd(a.ovf_cnt, 1)] = b;
     return;
+  }
+  if (!(a.flags & SH_FLAG_BUILD_ONLY)) {  // c4r: slots -> columns (path_l: the slot -> column table)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int sl = (w * K + k) * WAVE + lane;
+      if (sl < n) path_l[sl] = (int16_t)pk[k];
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += WG) c4r[i] = path_l[c4r[i]];
+    __syncthreads();
   }
   if constexpr (TIMED) {  // (col holds the segments: outputs without col)
     SantaArgs a2 = a;
@@ -5686,6 +5744,8 @@ int launch_santa_lb(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
     static_assert(2 * C::NW + 2 <= 63, "the step word's table field");
     const LbLds L = lb_lds_layout(a.n, ctx->ng, C::NW, C::K);
     if (L.total > 160 * 1024) return fail(SH_ERR_ARGS, "staged-row kernel: LDS above 160 KiB");
+    // (the slot sort's scratch: NCOL int16 slot entries in u's n int32)
+    if (C::NW * WAVE * C::K > 2 * a.n) return fail(SH_ERR_ARGS, "staged-row kernel: n too small for its config");
     static thread_local AttrCache attr;
     if (L.total > 64 * 1024 && attr.need(ctx->device, L.total)) {
       HIP_TRY(hipFuncSetAttribute((const void *)santa_lb_kernel<C::NW, C::K>,
