@@ -502,7 +502,7 @@ def assert_disjoint(rows: torch.Tensor, mode: int) -> None:
 _ZEROED = object()  # GPUEngine._zero_ev: the delta was zeroed on the round's stream
 
 
-def _wait_mail(mail, slot: int, seq: int, stream, spin: int = 256, poll: float = 20e-6,
+def _wait_mail(mail, slot: int, seq: int, stream, busy: float = 0.1, poll: float = 20e-6,
                check_every: float = 5e-3):
     """Wait for mailbox slot `slot` to carry sequence number `seq`, then
     return its (dS_child, dS_gift, None).  A bounded wait, not a spin
@@ -512,26 +512,30 @@ def _wait_mail(mail, slot: int, seq: int, stream, spin: int = 256, poll: float =
     so a sequence number still missing means the publish never happened (an
     announce/solve bookkeeping mismatch, a kernel that left early) and the
     wait raises instead of hanging.  Sequence numbers only grow per context:
-    a larger one in the slot means this round's value was overwritten."""
-    spins = 0
-    next_check = time.perf_counter() + check_every
+    a larger one in the slot means this round's value was overwritten.
+    The first `busy` seconds poll without sleeping: a round's publish lands
+    within milliseconds, and a sleep's wake-up (tens of microseconds to
+    milliseconds, by the host's timer slack) would be added to every round
+    (round 6: a 256-iteration spin then 20 us sleeps cost the 6-block
+    triplets round 1.5 -> 6.4 ms)."""
+    t0 = time.perf_counter()
+    next_check = t0 + check_every
     while True:
         got = mail[4 * slot]
         if got == seq:
             return int(mail[4 * slot + 1]), int(mail[4 * slot + 2]), None
         if got > seq:
             raise RuntimeError(f"mailbox slot {slot}: sequence {got} overwrote {seq} before it was read")
-        spins += 1
-        if spins <= spin:
-            continue
-        time.sleep(poll)
-        if time.perf_counter() >= next_check:
+        now = time.perf_counter()
+        if now >= next_check:
             # (query() raises a pending HIP error of the round's kernels; once
             #  it reports idle, the publish has landed if it ever will)
             if stream.query() and mail[4 * slot] != seq:
                 raise RuntimeError(f"mailbox slot {slot}: the round's stream is idle but sequence {seq} "
                                    f"was never published (slot holds {mail[4 * slot]})")
-            next_check = time.perf_counter() + check_every
+            next_check = now + check_every
+        if now - t0 > busy:
+            time.sleep(poll)
 
 
 def _wait(stream, ev) -> None:

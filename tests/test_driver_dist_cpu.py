@@ -409,11 +409,11 @@ def test_mailbox_wait_is_bounded():
     mail[4:8] = [7, 11, -3, 0]
     assert _wait_mail(mail, 1, 7, Stream()) == (11, -3, None)
     with pytest.raises(RuntimeError, match="never published"):
-        _wait_mail(mail, 0, 5, Stream(idle=True), spin=4, poll=1e-5, check_every=1e-4)
+        _wait_mail(mail, 0, 5, Stream(idle=True), busy=0.0, poll=1e-5, check_every=1e-4)
     with pytest.raises(RuntimeError, match="overwrote"):
         _wait_mail(mail, 1, 6, Stream())
     with pytest.raises(ValueError, match="HIP error"):
-        _wait_mail(mail, 0, 5, Stream(idle=False, exc=ValueError("HIP error")), spin=4, poll=1e-5,
+        _wait_mail(mail, 0, 5, Stream(idle=False, exc=ValueError("HIP error")), busy=0.0, poll=1e-5,
                    check_every=1e-4)
 
     class Late(Stream):  # the publish lands while the stream is still busy
@@ -422,4 +422,4 @@ def test_mailbox_wait_is_bounded():
             if self.calls == 3:
                 mail[0:3] = [9, 1, 2]
             return False
-    assert _wait_mail(mail, 0, 9, Late(), spin=4, poll=1e-5, check_every=1e-4) == (1, 2, None)
+    assert _wait_mail(mail, 0, 9, Late(), busy=0.0, poll=1e-5, check_every=1e-4) == (1, 2, None)
