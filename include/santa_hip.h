@@ -57,9 +57,11 @@ extern "C" {
 #define SH_FLAG_SW_TILE 16u     /* RETIRED (round 3): the one-wave register-
                                    tile kernel left the library; every entry
                                    point returns SH_ERR_ARGS for this flag */
-#define SH_FLAG_TIMING 64u      /* dev: the sparse kernel writes phase times
-                                   (wall-clock ticks since its start, 3 x 21
-                                   bits: built, solved, done) into d_steps */
+#define SH_FLAG_TIMING 64u      /* dev: the one-wave kernels (sparse, dense
+                                   tile), the staged-row and the 4-wave
+                                   kernels write wave 0's shader cycles per
+                                   solve segment into d_col instead of the
+                                   columns (see each kernel's TIMED note) */
 #define SH_FLAG_SP_TILE 128u    /* force the one-wave sparse kernel (the
                                    throughput design) even for few blocks  */
 #define SH_FLAG_SP1 256u        /* force the sparse kernel with LDS hit lists

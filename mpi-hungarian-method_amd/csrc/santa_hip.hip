@@ -3956,6 +3956,12 @@ __host__ __device__ __forceinline__ DtLds dt_lds_layout(int n, int ng) {
   return L;
 }
 
+// TIMED (SH_FLAG_TIMING, dev): wave 0's shader-clock cycles of the solve by
+// segment, written to col[b * n + q] instead of the columns: 0 A the step's
+// LDS group (row, dual, mover reads, the previous step's book-keeping),
+// 1 B relaxation + DPP argmin, 2 C decode to the next step, 3 D per-Dijkstra
+// (set-up, dual update, augmentation).
+template <bool TIMED = false>
 __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
   round_prologue(a, blockIdx.x, 0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -3998,6 +4004,15 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
   // folded into the step's scalar: a wish (c - nw1) * 512 and a miss 1 in
   // V units, i.e. a miss enters as MK = 2^11 + (nw1 << 20)
   const uint32_t MK = (uint32_t)SP3_MISS + ((uint32_t)nw1 << 20);
+  uint64_t tA = 0, tB = 0, tC = 0, tD = 0, ts = 0;
+  auto stamp = [&](uint64_t &acc) {
+    if constexpr (TIMED) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      acc += t - ts;
+      ts = t;
+    }
+  };
+  if constexpr (TIMED) ts = __builtin_amdgcn_s_memtime();
   uint32_t v20 = 20;  // (the SDWA shifts' amount, in a VGPR)
   asm volatile("" : "+v"(v20));
   uint32_t sbp[4];
@@ -4049,8 +4064,11 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       uint32_t kX = 0;
       uint32_t rpa = 0;   // the previous step's rem[pstar] address
       int mover_v = 0;    // its mover, stored by the group, then replaced by this step's
+      bool first = true;
       for (;;) {
         ++steps;
+        stamp(first ? tD : tC);
+        first = false;
         int32_t uraw;
         uint32_t w4;  // the codes of this lane's four columns in row i
         const uint32_t ua = ubase + 4u * (uint32_t)i;
@@ -4094,6 +4112,10 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
               "=&v"(tx)
             : "v"(ua), "v"(ra), "v"(ta), "s"(wmask), "s"(kw), "s"(mmask), "s"(kmv), "s"(kX), "v"(rpa)
             : "memory", "m0");
+        if constexpr (TIMED) {
+          asm volatile("" ::"v"(w4), "v"(uraw));
+          stamp(tA);
+        }
         const int32_t ui = __builtin_amdgcn_readfirstlane(uraw) - minVal;
         accU |= (uint32_t)ui + LR.CU;
         uint32_t bse = ((uint32_t)(SP3_BIAS - ui) << SP3_SH) - ((uint32_t)nw1 << 20) + (uint32_t)(n - nrem);
@@ -4123,6 +4145,10 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         }
         const uint32_t rsel = __builtin_amdgcn_ubfe(r4c, best << 3, 8);
         const uint32_t g = wave_min_u32_dpp(best);
+        if constexpr (TIMED) {
+          asm volatile("" ::"s"(g));
+          stamp(tB);
+        }
         minVal = (int32_t)(g >> SP3_SH) - SP3_BIAS;
         kw = (int)(g & 3u);
         const uint32_t pkey = (g >> 2) & 255u;
@@ -4141,6 +4167,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
         i = __builtin_amdgcn_readlane((int)rsel, lw);
         if (!assigned) break;
       }
+      stamp(tC);
       // dual update, path rows, augmentation: santa_sp3_kernel's
       const uint32_t mvb = (uint32_t)(minVal + SP3_BIAS);
       i32x4 prow;
@@ -4202,6 +4229,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       bad |= pi != cur;
     }
   }
+  stamp(tD);
   // the lattice range (see santa_sp3_kernel): leave the block to the fallback
   // launch (the outputs come from the tile, so the final duals need no check)
   if (__builtin_expect(__any(bad || ((accU & LR.MU) | (accW & LR.MW)) != 0), 0)) {
@@ -4224,7 +4252,7 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
       cost += single_cost(cn, nw1, E);
       dch += child_happy(cn, nw1) - child_happy(co, nw1);
       if (a.delta) dgh += gift_happy(a, chd, tnew) - gift_happy(a, chd, told);
-      if (a.col) a.col[(size_t)b * n + i] = col;
+      if (a.col && !TIMED) a.col[(size_t)b * n + i] = col;
       if (!(a.flags & SH_FLAG_NO_APPLY)) a.types[chd] = (int16_t)tnew;  // this block owns chd
     }
   }
@@ -4234,6 +4262,10 @@ __global__ __launch_bounds__(SANTA_WG) void santa_dt_kernel(SantaArgs a) {
   if (lane == 0) {
     if (a.cost) a.cost[b] = cost;
     if (a.steps) a.steps[b] = steps;
+    if (TIMED && a.col && n >= 4) {
+      const uint64_t seg[4] = {tA, tB, tC, tD};
+      for (int q = 0; q < 4; ++q) a.col[(size_t)b * n + q] = (int32_t)min(seg[q], (uint64_t)INT32_MAX);
+    }
     if (a.delta) {
       atomicAdd((unsigned long long *)&a.delta[0], (unsigned long long)dch);
       atomicAdd((unsigned long long *)&a.delta[1], (unsigned long long)dgh);
@@ -5850,18 +5882,27 @@ int launch_santa_dt(sh_ctx *ctx, SantaArgs a, int B, hipStream_t s) {
   if (ctx->n_wish > 253) return fail(SH_ERR_ARGS, "dense tile: n_wish > 253 does not fit the uint8 rank codes");
   const size_t lds = dt_lds_layout(a.n, ctx->ng).total;
   if (lds > 160 * 1024) return fail(SH_ERR_ARGS, "dense tile: too many gift types for LDS");
-  static thread_local AttrCache attr;
+  static thread_local AttrCache attr, attr_t;
   if (lds > 64 * 1024 && attr.need(ctx->device, lds)) {
-    HIP_TRY(hipFuncSetAttribute((const void *)santa_dt_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIP_TRY(hipFuncSetAttribute((const void *)santa_dt_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
     attr.set(ctx->device, lds);
+  }
+  const bool timed = (a.flags & SH_FLAG_TIMING) != 0;
+  if (timed && lds > 64 * 1024 && attr_t.need(ctx->device, lds)) {
+    HIP_TRY(hipFuncSetAttribute((const void *)santa_dt_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    attr_t.set(ctx->device, lds);
   }
   HIP_TRY_RC(ensure_ovf(ctx, B, s));
   const int p = ctx->ovf_par;
   a.ovf_cnt = ctx->d_ovf + p;
   a.ovf_list = ctx->d_ovf + 2 + (size_t)p * ctx->ovf_cap;
   a.blist = nullptr;
-  hipLaunchKernelGGL(santa_dt_kernel, dim3(B), dim3(SANTA_WG), lds, s, a);
+  if (timed)
+    hipLaunchKernelGGL(santa_dt_kernel<true>, dim3(B), dim3(SANTA_WG), lds, s, a);
+  else
+    hipLaunchKernelGGL(santa_dt_kernel<false>, dim3(B), dim3(SANTA_WG), lds, s, a);
   HIP_TRY(hipGetLastError());
   SantaArgs f = a;
   f.blist = a.ovf_list;
@@ -5984,8 +6025,8 @@ int dt_tile_slots(sh_ctx *ctx, int n) {
   const size_t lds = dt_lds_layout(n, ctx->ng).total;
   if (lds <= 160 * 1024) {
     if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute((const void *)santa_dt_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, santa_dt_kernel, SANTA_WG, lds) != hipSuccess)
+      (void)hipFuncSetAttribute((const void *)santa_dt_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, santa_dt_kernel<false>, SANTA_WG, lds) != hipSuccess)
       per_cu = 0;
   }
   ctx->dt_slots = per_cu * ctx->n_cu;

@@ -26,8 +26,9 @@ def main():
     ap.add_argument("--budget", type=int, default=0, help="sparse kernel LDS bytes per block (0 = default)")
     ap.add_argument("--timing", action="store_true", help="per-phase in-kernel timing (sparse kernel)")
     ap.add_argument("--segments", action="store_true",
-                    help="santa_sp3_kernel: shader cycles per Dijkstra step by segment (A fetch+scatter+LDS, "
-                         "B relax+argmin, C decode+book-keeping, D per-Dijkstra work per step)")
+                    help="santa_sp3_kernel (santa_dt_kernel with --flags 4096): shader cycles per Dijkstra step "
+                         "by segment (A fetch+scatter+LDS, B relax+argmin, C decode+book-keeping, "
+                         "D per-Dijkstra work per step)")
     ap.add_argument("--lb-segments", action="store_true",
                     help="santa_lb_kernel (n > 256 singles): cycles per step by segment, per wave "
                          "(0 relax, 1 wave min, 2 candidate + staging + fold, 3 barrier, 4 decode, "
@@ -98,7 +99,9 @@ def main():
         sv = steps.cpu().numpy().astype(float)
         imax = int(sv.argmax())
         names = ["A_fetch_scatter_lds", "B_relax_argmin", "C_decode_bookkeeping", "D_per_dijkstra"]
-        if a.mode == 1:  # (the 4-wave twins kernel, sap_solve_mw_sc: wave 0's segments)
+        if a.flags & 4096:  # (santa_dt_kernel, forced by SH_FLAG_DT_TILE)
+            names = ["A_lds_group", "B_relax_argmin", "C_decode", "D_per_dijkstra"]
+        elif a.mode == 1:  # (the 4-wave twins kernel, sap_solve_mw_sc: wave 0's segments)
             names = ["A_dual_row_loads", "B_relax_rowmin_fold", "C_barrier", "D_word_decode", "E_per_dijkstra"]
         elif (a.flags & 8) == 0:  # (santa_sp3_kernel: A split at the LDS issue, A1 = tile fetch + fields)
             names = ["A2_lds_bookkeeping", "B_relax_argmin", "C_decode", "D0_setup", "A1_tile_fetch",
